@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/ from the REFERENCE itself (oracle/_ref/, built by
+`make -C oracle/ref` from the unmodified sources under /root/reference).
+
+Run in the build container only (it needs the reference build):
+    make -C oracle/ref && make -C oracle && python3 oracle/gen_golden.py
+
+Every fixture is data: inputs (seeds, plane specs, dt) and the outputs the
+reference produced for them. The oracle restatement (df_oracle.c) is then
+required to reproduce these bit for bit (tests/test_oracle_golden.py).
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+REF = os.path.join(HERE, "_ref")
+HARN = os.path.join(REF, "ref_harness")
+RUN_ROOT = os.path.join(REF, "run_root")
+OUT = os.path.join(ROOT, "tests", "golden")
+FIELDS = ("u", "v", "w", "T", "rho")
+ROWS = ("R11", "R21", "R22", "R33", "Us", "Ts", "rhos", "Ms")
+KAT = "/root/reference/digital-filtering-c++/pcg-cpp/test-high/expected/check-pcg32.out"
+
+sys.path.insert(0, HERE)
+import oracle as O  # noqa: E402  (only to record the derived stream start state)
+
+
+def run(*args):
+    subprocess.run([HARN, *map(str, args)], check=True, stdout=subprocess.DEVNULL)
+
+
+def stats(a):
+    return np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
+
+
+def load_case(d, Ny, Nz, nsteps):
+    meta = json.load(open(os.path.join(d, "meta.json")))
+    rows = {r: np.fromfile(os.path.join(d, r + ".bin")) for r in ROWS}
+    Ns = {}
+    for c in "uvw":
+        for dn in "yz":
+            a = np.fromfile(os.path.join(d, f"N{dn}s_{c}.bin"), dtype=np.int32).reshape(meta["Ny"], meta["Nz"])
+            assert (a == a[:, :1]).all(), "half-width is not uniform along a row"
+            Ns[f"N{dn}_{c}"] = a[:, 0].copy()
+    steps = []
+    for s in range(nsteps + 1):
+        steps.append({k: np.fromfile(os.path.join(d, f"step{s}_{k}.bin")).reshape(meta["Ny"], meta["Nz"])
+                      for k in FIELDS})
+    return meta, rows, Ns, steps
+
+
+def kat():
+    lines = [l.rstrip("\r\n") for l in open(KAT)]
+    r1 = lines.index("Round 1:")
+    first = [int(x, 16) for x in lines[r1 + 1].split(":")[1].split()]
+    again = [int(x, 16) for x in lines[r1 + 2].split(":")[1].split()]
+    coins = lines[r1 + 3].split(":")[1].strip()
+    json.dump({"source": "pcg-cpp/test-high/expected/check-pcg32.out (reference's own KAT)",
+               "seed": 42, "stream": 54, "round1_32bit": first, "round1_again": again,
+               "round1_coins": coins}, open(os.path.join(OUT, "pcg32_kat.json"), "w"), indent=1)
+
+
+def rng_fixture(seed, n=4096):
+    with tempfile.TemporaryDirectory() as d:
+        run("rng", seed, n, d)
+        u = np.fromfile(os.path.join(d, "u32.bin"), dtype=np.uint32)
+        g = np.fromfile(os.path.join(d, "normals.bin"))
+    np.savez_compressed(os.path.join(OUT, f"rng_s{seed}.npz"), seed=seed, u32=u, normals=g)
+
+
+def native_fixture(seed=42, dt=1e-8, nsteps=2, sample_rows=(1, 100, 300, 509)):
+    with tempfile.TemporaryDirectory() as d:
+        run("native", RUN_ROOT, seed, dt, nsteps, d)
+        meta, rows, Ns, steps = load_case(d, 0, 0, nsteps)
+    arr = {"seed": seed, "dt": dt, "nsteps": nsteps, "sample_rows": np.array(sample_rows)}
+    arr.update({f"row_{k}": v for k, v in rows.items()})
+    arr.update(Ns)
+    for s, st in enumerate(steps):
+        for k in FIELDS:
+            arr[f"s{s}_{k}_stats"] = stats(st[k])
+            arr[f"s{s}_{k}_rows"] = st[k][list(sample_rows)]
+    np.savez_compressed(os.path.join(OUT, f"native_s{seed}.npz"), **arr)
+    json.dump(meta, open(os.path.join(OUT, f"native_s{seed}.json"), "w"), indent=1)
+
+
+def synth_fixture(name, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, dt2=None, nsteps2=0, full_steps=(),
+                  sample_rows=None, csv_head=0):
+    with tempfile.TemporaryDirectory() as d:
+        extra = [dt2, nsteps2] if nsteps2 else []
+        run("synth", RUN_ROOT, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, d, *extra)
+        meta, rows, Ns, steps = load_case(d, Ny, Nz, nsteps + nsteps2)
+        if csv_head:
+            with open(os.path.join(RUN_ROOT, "files", "cpp_vel_fluc.csv")) as f:
+                head = [next(f) for _ in range(csv_head)]
+            open(os.path.join(OUT, f"{name}_csv_head.txt"), "w").writelines(head)
+    # The reference runs its native constructor first (one process-wide static
+    # stream, df.cpp:334-335); record where the synthetic plane's stream starts.
+    rng = O.Rng(seed=seed)
+    O.Filter(rng=rng)
+    st, flag, saved = rng.state
+    sample_rows = sample_rows or (0, 1, Ny // 4, Ny // 2, Ny - 1)
+    arr = {"seed": seed, "Ny": Ny, "Nz": Nz, "N_min": Nmin, "N_max": Nmax, "dt": dt, "nsteps": nsteps,
+           "dt2": dt2 if dt2 is not None else 0.0, "nsteps2": nsteps2,
+           "start_state": np.uint64(st), "start_saved_flag": flag, "start_saved": saved,
+           "sample_rows": np.array(sample_rows), "full_steps": np.array(full_steps, dtype=np.int64)}
+    arr.update({f"row_{k}": v for k, v in rows.items()})
+    arr.update(Ns)
+    for s, stp in enumerate(steps):
+        for k in FIELDS:
+            arr[f"s{s}_{k}_stats"] = stats(stp[k])
+            arr[f"s{s}_{k}_rows"] = stp[k][list(sample_rows)]
+            if s in full_steps:
+                arr[f"s{s}_{k}"] = stp[k]
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arr)
+    json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=1)
+
+
+def main():
+    if not os.path.exists(HARN):
+        sys.exit("reference not built: make -C oracle/ref")
+    os.makedirs(OUT, exist_ok=True)
+    kat()
+    rng_fixture(42)
+    rng_fixture(1234)
+    native_fixture()
+    # c1: 128x128, constant N = 8 (BASELINE configs[0]); 3 x filter(1e-8) then filter(1e-5)
+    synth_fixture("c1_s42", 42, 128, 128, 8, 8, 1e-8, 3, dt2=1e-5, nsteps2=1, full_steps=(3,),
+                  csv_head=12)
+    # small ramp-rule plane (SURVEY §8d rule, N in [4,16]) on another seed
+    synth_fixture("ramp256_s1234", 1234, 256, 256, 4, 16, 1e-8, 2)
+    # ragged plane: odd sizes, Nz smaller than the largest half-width
+    synth_fixture("ragged_s7", 7, 37, 5, 2, 10, 1e-8, 2, full_steps=(0, 2), sample_rows=(0, 18, 36))
+    manifest = {
+        "generator": "oracle/gen_golden.py",
+        "reference": "connorswitala/digital-filtering @ /root/reference (df.cpp compiled unmodified, "
+                     "g++ -std=c++17 -O2, -include oracle/ref/ref_shim.hpp)",
+        "compiler": subprocess.run(["g++", "--version"], capture_output=True, text=True).stdout.splitlines()[0],
+        "files": sorted(os.listdir(OUT)),
+    }
+    json.dump(manifest, open(os.path.join(OUT, "MANIFEST.json"), "w"), indent=1)
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()

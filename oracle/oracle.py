@@ -1,0 +1,220 @@
+"""ORACLE — test infrastructure only.
+
+ctypes view of oracle/liboracle.so (the plain-C restatement in df_oracle.c).
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this,
+and only as the checker. The product (digital-filtering_amd/) never does.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DATA = os.path.join(os.path.dirname(HERE), "digital-filtering_amd", "data")
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+
+PLANE_NATIVE, PLANE_SYNTHETIC = 0, 1
+
+
+class _Rng(C.Structure):
+    _fields_ = [("state", C.c_uint64), ("saved_flag", C.c_int), ("saved", C.c_double),
+                ("attempts", C.c_uint64), ("accepted", C.c_uint64)]
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("plane", C.c_int), ("Ny", C.c_int), ("Nz", C.c_int), ("N_min", C.c_int),
+                ("N_max", C.c_int), ("rst_file", C.c_char_p), ("line_file", C.c_char_p)]
+
+
+class _Field(C.Structure):
+    _fields_ = [("by", C.POINTER(C.c_double)), ("bz", C.POINTER(C.c_double)),
+                ("r_ys", C.POINTER(C.c_double)), ("r_zs", C.POINTER(C.c_double)),
+                ("filt_old", C.POINTER(C.c_double)), ("filt", C.POINTER(C.c_double)),
+                ("fluc", C.POINTER(C.c_double)),
+                ("N_ys", C.POINTER(C.c_int)), ("N_zs", C.POINTER(C.c_int)),
+                ("by_offsets", C.POINTER(C.c_int)), ("bz_offsets", C.POINTER(C.c_int)),
+                ("by_size", C.c_longlong), ("bz_size", C.c_longlong),
+                ("r_ys_size", C.c_longlong), ("r_zs_size", C.c_longlong),
+                ("Iz_inn", C.c_double), ("Iz_out", C.c_double), ("Lt", C.c_double),
+                ("Nz_max", C.c_int), ("Ny_max", C.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"oracle not built: {LIB_PATH} (run `make -C oracle`)")
+        L = C.CDLL(LIB_PATH)
+        L.orc_pcg32_seed1.restype = C.c_uint64
+        L.orc_pcg32_seed1.argtypes = [C.c_uint64]
+        L.orc_pcg32_seed2.argtypes = [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.orc_pcg32_next.restype = C.c_uint32
+        L.orc_pcg32_next.argtypes = [C.POINTER(C.c_uint64), C.c_uint64]
+        L.orc_pcg32_advance.restype = C.c_uint64
+        L.orc_pcg32_advance.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        L.orc_pcg32_fill.argtypes = [C.POINTER(C.c_uint64), C.c_uint64, C.c_void_p, C.c_size_t]
+        L.orc_rng_seed.argtypes = [C.POINTER(_Rng), C.c_uint64]
+        L.orc_normals.argtypes = [C.POINTER(_Rng), C.c_void_p, C.c_size_t]
+        L.orc_df_create.restype = C.c_void_p
+        L.orc_df_create.argtypes = [C.POINTER(_Cfg), C.POINTER(_Rng)]
+        L.orc_df_destroy.argtypes = [C.c_void_p]
+        L.orc_last_error.restype = C.c_char_p
+        for fn in ("orc_generate_white_noise", "orc_apply_RST_scaling", "orc_get_rho_T_fluc"):
+            getattr(L, fn).argtypes = [C.c_void_p]
+        L.orc_filtering_sweeps.argtypes = [C.c_void_p, C.c_int]
+        L.orc_correlate_fields.argtypes = [C.c_void_p, C.c_int]
+        L.orc_filter.argtypes = [C.c_void_p, C.c_double]
+        L.orc_field_ptr.restype = C.POINTER(C.c_double)
+        L.orc_field_ptr.argtypes = [C.c_void_p, C.c_int]
+        L.orc_dims.restype = C.c_int
+        L.orc_dims.argtypes = [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+        L.orc_row_ptr.restype = C.POINTER(C.c_double)
+        L.orc_row_ptr.argtypes = [C.c_void_p, C.c_int]
+        L.orc_field_struct.restype = C.POINTER(_Field)
+        L.orc_field_struct.argtypes = [C.c_void_p, C.c_int]
+        L.orc_scalar.restype = C.c_double
+        L.orc_scalar.argtypes = [C.c_void_p, C.c_int]
+        L.orc_write_csv.restype = C.c_int
+        L.orc_write_csv.argtypes = [C.c_void_p, C.c_char_p]
+        L.orc_synthetic_N.restype = C.c_int
+        L.orc_synthetic_N.argtypes = [C.c_int] * 4
+        _lib = L
+    return _lib
+
+
+# ----------------------------------------------------------------- pcg32
+
+def pcg32_seed1(seed):
+    return lib().orc_pcg32_seed1(seed)
+
+
+def pcg32_u32(seed, n, state=None):
+    """First n outputs of pcg32{seed} (1-arg ctor) or from an explicit state."""
+    st = C.c_uint64(pcg32_seed1(seed) if state is None else state)
+    out = np.empty(n, dtype=np.uint32)
+    lib().orc_pcg32_fill(C.byref(st), 1442695040888963407, out.ctypes.data, n)
+    return out, st.value
+
+
+def pcg32_fill(state, inc, n):
+    st = C.c_uint64(state)
+    out = np.empty(n, dtype=np.uint32)
+    lib().orc_pcg32_fill(C.byref(st), inc, out.ctypes.data, n)
+    return out, st.value
+
+
+def pcg32_seed2_u32(seed, stream, n):
+    st, inc = C.c_uint64(), C.c_uint64()
+    lib().orc_pcg32_seed2(seed, stream, C.byref(st), C.byref(inc))
+    out = np.empty(n, dtype=np.uint32)
+    lib().orc_pcg32_fill(C.byref(st), inc.value, out.ctypes.data, n)
+    return out, st.value, inc.value
+
+
+def pcg32_advance(state, delta, inc=1442695040888963407):
+    return lib().orc_pcg32_advance(state, delta % (1 << 64), inc)
+
+
+class Rng:
+    """libstdc++-11 normal_distribution<double> over pcg32 (the reference's stream)."""
+
+    def __init__(self, seed=None, state=None, saved_flag=0, saved=0.0):
+        self._r = _Rng()
+        if seed is not None:
+            lib().orc_rng_seed(C.byref(self._r), seed)
+        else:
+            self._r.state, self._r.saved_flag, self._r.saved = state, saved_flag, saved
+
+    def normals(self, n):
+        out = np.empty(n, dtype=np.float64)
+        lib().orc_normals(C.byref(self._r), out.ctypes.data, n)
+        return out
+
+    @property
+    def state(self):
+        return (self._r.state, self._r.saved_flag, self._r.saved)
+
+    @property
+    def attempts(self):
+        return self._r.attempts
+
+
+# ------------------------------------------------------------- the filter
+
+FIELDS = ("u", "v", "w", "T", "rho")
+ROWS = ("R11", "R21", "R22", "R33", "Us", "Ts", "rhos", "Ms", "Ps", "yline", "ydline")
+
+
+class Filter:
+    """Oracle DIGITAL_FILTER. The constructor runs setup + step 0 like df.cpp:4-66."""
+
+    def __init__(self, plane=PLANE_NATIVE, Ny=0, Nz=0, N_min=0, N_max=0, rng=None, seed=42,
+                 rst_file=None, line_file=None):
+        self.rng = rng if rng is not None else Rng(seed=seed)
+        self._cfg = _Cfg(plane, Ny, Nz, N_min, N_max,
+                         (rst_file or os.path.join(DATA, "RST.dat")).encode(),
+                         (line_file or os.path.join(DATA, "line.dat")).encode())
+        self._h = lib().orc_df_create(C.byref(self._cfg), C.byref(self.rng._r))
+        if not self._h:
+            raise RuntimeError(lib().orc_last_error().decode())
+        ny, nz = C.c_int(), C.c_int()
+        lib().orc_dims(self._h, C.byref(ny), C.byref(nz))
+        self.Ny, self.Nz = ny.value, nz.value
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().orc_df_destroy(h)
+            self._h = None
+
+    def filter(self, dt):
+        lib().orc_filter(self._h, dt)
+
+    def field(self, name):
+        i = FIELDS.index(name)
+        p = lib().orc_field_ptr(self._h, i)
+        return np.ctypeslib.as_array(p, shape=(self.Ny, self.Nz)).copy()
+
+    def fields(self):
+        return {k: self.field(k) for k in FIELDS}
+
+    def row(self, name):
+        p = lib().orc_row_ptr(self._h, ROWS.index(name))
+        return np.ctypeslib.as_array(p, shape=(self.Ny,)).copy()
+
+    def comp(self, c):
+        return lib().orc_field_struct(self._h, c).contents
+
+    def halfwidths(self, c, direction):
+        F = self.comp(c)
+        p = F.N_ys if direction == "y" else F.N_zs
+        return np.ctypeslib.as_array(p, shape=(self.Ny, self.Nz)).copy()
+
+    def scalar(self, name):
+        return lib().orc_scalar(self._h, ("u_tau", "tau_w", "d_v").index(name))
+
+    def write_csv(self, path):
+        return lib().orc_write_csv(self._h, path.encode())
+
+    # stage-wise access (df.hpp:92-102 public member functions)
+    def generate_white_noise(self):
+        lib().orc_generate_white_noise(self._h)
+
+    def filtering_sweeps(self, c):
+        lib().orc_filtering_sweeps(self._h, c)
+
+
+def synthetic_N(j, Ny, N_min, N_max):
+    return lib().orc_synthetic_N(j, Ny, N_min, N_max)
+
+
+def stream_lengths(f):
+    """Normals drawn per filter() call, in stream order (df.cpp:343-348)."""
+    out = []
+    for c in range(3):
+        F = f.comp(c)
+        out += [F.r_ys_size, F.r_zs_size]
+    return out

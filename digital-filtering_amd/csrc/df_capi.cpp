@@ -1,0 +1,937 @@
+// C ABI of libdfamd.so (include/df_c.h): host orchestration of the MI355X
+// filter(dt) path. One handle = one GPU = one z-strip of the inflow plane.
+//
+// Per df_filter call (reference df.cpp:449-468), all on the handle's stream:
+//   rng_count -> rng_scan -> rng_generate      generate_white_noise (332-349)
+//   ypass (u,v,w in one launch)                filtering_sweeps y-part (359-383)
+//   [halo pack -> RCCL send/recv -> unpack]    only when the plane is split
+//   zpass_epilogue (u,v,w in one launch)       z-part (385-405) + correlate_fields
+//                                              (408-417) + apply_RST_scaling
+//                                              (419-447) + get_rho_T_fluc (470-485)
+#include "df_c.h"
+#include "df_kernels.hpp"
+#include "df_rng.hpp"
+#include "df_setup.hpp"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+using namespace dfamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_OR(expr, code)                                                                                  \
+    do {                                                                                                    \
+        hipError_t e_ = (expr);                                                                             \
+        if (e_ != hipSuccess) return fail(code, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+    } while (0)
+
+#define NCCL_OR(expr)                                                                                       \
+    do {                                                                                                    \
+        ncclResult_t r_ = (expr);                                                                           \
+        if (r_ != ncclSuccess) return fail(DF_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(r_));   \
+    } while (0)
+
+struct CompDev {
+    int Nyp = 0, Nzp = 0, rz_pitch = 0;
+    double *ry = nullptr, *rz = nullptr, *By = nullptr, *Bz = nullptr;
+    long long *byoff = nullptr, *bzoff = nullptr;
+    int *Ny_row = nullptr, *Nz_row = nullptr;
+    double *filt_old = nullptr, *fluc = nullptr, *filt = nullptr;
+    long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
+    long long by_size = 0, bz_size = 0;   // reference offset-packed sizes (this strip's cells)
+    double sa = 0, s1a = 0;
+};
+
+struct PhaseEvents {
+    hipEvent_t e[5];
+};
+
+} // namespace
+
+struct df_handle {
+    Flow flow;
+    PlaneSpec spec;
+    Setup setup;
+    int coeff_mode = DF_COEFF_PACKED;
+    std::string csv_path;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int rank = 0, world = 1;
+    ncclComm_t comm = nullptr;
+    int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
+    int rows_per_wave = 8;
+    CompDev c[3];
+    double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr;
+    int *tab_off = nullptr;
+    // RNG
+    RngStateDev *rstate = nullptr; // [2], ping-pong by call parity
+    int *counts = nullptr;
+    long long *offsets = nullptr;
+    int *err_dev = nullptr;   // mapped host memory
+    int *err_host = nullptr;
+    int rng_blocks = 0;
+    long long calls = 0;      // RNG generations so far (selects the ping-pong slot)
+    RngGeom geom{};
+    // halo
+    double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
+    size_t halo_elems = 0;
+    // profiling
+    bool profiling = false;
+    std::vector<PhaseEvents> ev;
+    size_t ev_used = 0;
+    df_profile prof{};
+    std::vector<void *> allocs;
+};
+
+namespace {
+
+int dalloc(df_handle *h, void **p, size_t bytes)
+{
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess)
+        return fail(e == hipErrorOutOfMemory ? DF_ENOMEM : DF_EHIP,
+                    "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    h->allocs.push_back(*p);
+    HIP_OR(hipMemsetAsync(*p, 0, bytes, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+template <class T> int dalloc_t(df_handle *h, T **p, size_t n) { return dalloc(h, (void **)p, n * sizeof(T)); }
+
+template <class T> int upload(df_handle *h, T *dst, const T *src, size_t n)
+{
+    HIP_OR(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP); // src may be a temporary
+    return DF_OK;
+}
+
+SweepArgs sweep_args(df_handle *h)
+{
+    SweepArgs a{};
+    for (int c = 0; c < 3; ++c) {
+        CompDev &d = h->c[c];
+        a.ry[c] = d.ry;
+        a.rz[c] = d.rz;
+        a.By[c] = d.By;
+        a.Bz[c] = d.Bz;
+        a.byoff[c] = d.byoff;
+        a.bzoff[c] = d.bzoff;
+        a.Ny_row[c] = d.Ny_row;
+        a.Nz_row[c] = d.Nz_row;
+        a.Nyp[c] = d.Nyp;
+        a.Nzp[c] = d.Nzp;
+        a.rz_pitch[c] = d.rz_pitch;
+        a.filt_old[c] = d.filt_old;
+        a.fluc[c] = d.fluc;
+        a.filt[c] = d.filt;
+        a.sa[c] = d.sa;
+        a.s1a[c] = d.s1a;
+    }
+    a.Ny = h->Ny;
+    a.Nz_loc = h->Nz_loc;
+    a.Pz = h->Pz;
+    a.nstrips = h->nstrips;
+    a.tab = h->tab;
+    a.tab_off = h->tab_off;
+    a.T = h->T;
+    a.rho = h->rho;
+    a.rowc = h->rowc;
+    a.comps_mask = 7;
+    return a;
+}
+
+int check_rng_error(df_handle *h)
+{
+    if (h->err_host && *(volatile int *)h->err_host)
+        return fail(DF_ERNG, "device RNG ran short of polar attempts; stream state is invalid");
+    return DF_OK;
+}
+
+void ev_record(df_handle *h, int phase)
+{
+    if (!h->profiling) return;
+    if (h->ev_used >= h->ev.size()) return;
+    (void)hipEventRecord(h->ev[h->ev_used].e[phase], h->stream);
+}
+
+int drain_profile(df_handle *h)
+{
+    if (!h->ev_used) return DF_OK;
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    for (size_t i = 0; i < h->ev_used; ++i) {
+        float t[4] = {0, 0, 0, 0}, tot = 0;
+        for (int p = 0; p < 4; ++p) (void)hipEventElapsedTime(&t[p], h->ev[i].e[p], h->ev[i].e[p + 1]);
+        (void)hipEventElapsedTime(&tot, h->ev[i].e[0], h->ev[i].e[4]);
+        h->prof.rng_ms += t[0];
+        h->prof.ypass_ms += t[1];
+        h->prof.halo_ms += t[2];
+        h->prof.zpass_ms += t[3];
+        h->prof.total_ms += tot;
+        h->prof.calls++;
+    }
+    h->ev_used = 0;
+    return DF_OK;
+}
+
+// ---------------------------------------------------------------- phases
+
+int phase_rng(df_handle *h)
+{
+    const int in = (int)(h->calls & 1), out = in ^ 1;
+    HIP_OR(launch_rng(h->geom, h->rstate + in, h->rstate + out, h->counts, h->offsets, h->err_dev, h->rng_blocks,
+                      h->stream),
+           DF_EHIP);
+    h->calls++;
+    return DF_OK;
+}
+
+int phase_ypass(df_handle *h, int comps_mask)
+{
+    SweepArgs a = sweep_args(h);
+    a.comps_mask = comps_mask;
+    HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+int phase_halo_pack(df_handle *h)
+{
+    if (h->world == 1) return DF_OK;
+    SweepArgs a = sweep_args(h);
+    HIP_OR(launch_halo_pack(a, h->rank > 0 ? h->send_l : nullptr, h->rank < h->world - 1 ? h->send_r : nullptr,
+                            h->stream),
+           DF_EHIP);
+    return DF_OK;
+}
+
+int phase_halo_unpack(df_handle *h)
+{
+    if (h->world == 1) return DF_OK;
+    SweepArgs a = sweep_args(h);
+    HIP_OR(launch_halo_unpack(a, h->rank > 0 ? h->recv_l : nullptr, h->rank < h->world - 1 ? h->recv_r : nullptr,
+                              h->stream),
+           DF_EHIP);
+    return DF_OK;
+}
+
+int phase_halo_rccl(df_handle *h)
+{
+    if (h->world == 1) return DF_OK;
+    if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
+    int rc = phase_halo_pack(h);
+    if (rc) return rc;
+    NCCL_OR(ncclGroupStart());
+    if (h->rank > 0) {
+        NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, h->stream));
+        NCCL_OR(ncclRecv(h->recv_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, h->stream));
+    }
+    if (h->rank < h->world - 1) {
+        NCCL_OR(ncclSend(h->send_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, h->stream));
+        NCCL_OR(ncclRecv(h->recv_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, h->stream));
+    }
+    NCCL_OR(ncclGroupEnd());
+    return phase_halo_unpack(h);
+}
+
+int phase_zpass(df_handle *h, bool corr, bool sra, double dt)
+{
+    SweepArgs a = sweep_args(h);
+    if (corr) {
+        const double pi = 3.141592654; // df.cpp:411
+        for (int c = 0; c < 3; ++c) {
+            const double alpha = std::exp(-pi * dt / h->setup.comp[c].Lt);
+            a.sa[c] = std::sqrt(alpha);
+            a.s1a[c] = std::sqrt(1.0 - alpha);
+        }
+    }
+    a.do_corr = corr ? 1 : 0;
+    a.do_sra = sra ? 1 : 0;
+    HIP_OR(launch_zpass(a, h->coeff_mode == DF_COEFF_TABLE, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+int write_csv_if(df_handle *h)
+{
+    if (h->csv_path.empty()) return DF_OK;
+    const size_t n = (size_t)h->Ny * h->Nz_loc;
+    std::vector<double> f[5];
+    double *src[5] = {h->c[0].fluc, h->c[1].fluc, h->c[2].fluc, h->T, h->rho};
+    for (int i = 0; i < 5; ++i) {
+        f[i].resize(n);
+        HIP_OR(hipMemcpyAsync(f[i].data(), src[i], n * 8, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    }
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    std::string path = h->csv_path;
+    if (h->world > 1) path += ".rank" + std::to_string(h->rank);
+    std::string err;
+    if (!write_csv(h->setup, path, f[0].data(), f[1].data(), f[2].data(), f[3].data(), f[4].data(), h->z0,
+                   h->Nz_loc, err))
+        return fail(DF_EIO, err);
+    return DF_OK;
+}
+
+// ---------------------------------------------------------------- create
+
+int build(df_handle *h, const df_config_c *cfg)
+{
+    h->flow.d_i = cfg->d_i;
+    h->flow.rho_e = cfg->rho_e;
+    h->flow.U_e = cfg->U_e;
+    h->flow.mu = cfg->mu_e;
+    h->spec.kind = cfg->plane;
+    h->spec.Ny = cfg->Ny;
+    h->spec.Nz = cfg->Nz;
+    h->spec.N_min = cfg->N_min;
+    h->spec.N_max = cfg->N_max;
+    if (!cfg->vel_fluc_file || !cfg->line_file)
+        return fail(DF_EINVAL, "vel_fluc_file (RST profile) and line_file (mean profile) are required");
+    h->spec.rst_file = cfg->vel_fluc_file;
+    h->spec.line_file = cfg->line_file;
+    h->coeff_mode = cfg->coeff_mode;
+    if (h->coeff_mode != DF_COEFF_PACKED && h->coeff_mode != DF_COEFF_TABLE)
+        return fail(DF_EINVAL, "coeff_mode must be DF_COEFF_PACKED or DF_COEFF_TABLE");
+    if (cfg->csv_path) h->csv_path = cfg->csv_path;
+    h->rank = cfg->rank;
+    h->world = cfg->world < 1 ? 1 : cfg->world;
+    if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
+    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : 8;
+    if (h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 && h->rows_per_wave != 8)
+        return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
+
+    std::string err;
+    if (!build_setup(h->flow, h->spec, h->setup, err)) return fail(DF_EIO, err);
+    Setup &s = h->setup;
+
+    // ---- partition (host)
+    h->Ny = s.Ny;
+    h->Nz_g = s.Nz;
+    h->z0 = (int)((long long)h->rank * s.Nz / h->world);
+    h->z1 = (int)((long long)(h->rank + 1) * s.Nz / h->world);
+    h->Nz_loc = h->z1 - h->z0;
+    if (h->Nz_loc < 1) return fail(DF_EINVAL, "more z-strips than plane columns");
+    h->nstrips = (h->Nz_loc + kStrip - 1) / kStrip;
+    h->Pz = h->nstrips * kStrip;
+    for (int c = 0; c < 3; ++c)
+        if (h->world > 1 && s.comp[c].Nz_max > h->Nz_loc)
+            return fail(DF_EINVAL, "z-strip narrower than the z half-width: use fewer GPUs");
+    const int Ny = s.Ny;
+    for (int c = 0; c < 3; ++c) {
+        CompDev &d = h->c[c];
+        const ComponentSetup &F = s.comp[c];
+        d.Nyp = F.Ny_max;
+        d.Nzp = F.Nz_max;
+        d.rz_pitch = h->Pz + 2 * d.Nzp;
+        d.by_size = d.bz_size = 0;
+        for (int j = 0; j < Ny; ++j) {
+            d.by_size += (long long)h->Nz_loc * (2 * F.Ny_row[j] + 1);
+            d.bz_size += (long long)h->Nz_loc * (2 * F.Nz_row[j] + 1);
+        }
+    }
+
+    // ---- RNG stream geometry (df.cpp:343-348 order) and launch size
+    RngGeom &g = h->geom;
+    g.seg[0] = 0;
+    for (int c = 0; c < 3; ++c) {
+        const uint64_t Ly = (uint64_t)s.Nz * (Ny + 2 * h->c[c].Nyp);
+        const uint64_t Lz = (uint64_t)Ny * (s.Nz + 2 * h->c[c].Nzp);
+        if (Ly >= (1ull << 32) || Lz >= (1ull << 32)) return fail(DF_EINVAL, "noise array exceeds 2^32 normals");
+        g.seg[2 * c + 1] = g.seg[2 * c] + Ly;
+        g.seg[2 * c + 2] = g.seg[2 * c + 1] + Lz;
+    }
+    g.Q = g.seg[6];
+    const PcgJump hop = pcg_jump(4ull * (kRngThreads - 1));
+    g.hop_mult = hop.mult;
+    g.hop_plus = hop.plus;
+    g.Nz_g = s.Nz;
+    g.Pz = h->Pz;
+    g.z0 = h->z0;
+    g.z1 = h->z1;
+    g.is_first = h->rank == 0;
+    g.is_last = h->rank == h->world - 1;
+    {
+        const double A = std::ceil((double)g.Q / 2.0);
+        const double p = 0.78539816339744830962; // pi/4 acceptance of the polar method
+        const double T = A / p * 1.002 + 16.0 * std::sqrt(A) + 8192.0;
+        h->rng_blocks = (int)std::ceil(T / kRngBlockAttempts);
+    }
+    if (cfg->device < 0) { // host-only handle: setup queries, no GPU
+        h->device = -1;
+        return DF_OK;
+    }
+
+    // ---- device
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(DF_EHIP, "no HIP device visible");
+    if (cfg->device >= ndev) return fail(DF_EINVAL, "device ordinal out of range");
+    h->device = cfg->device;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), DF_EHIP);
+
+    // ---- per-N coefficient table
+    std::vector<int> tab_off_h;
+    std::vector<double> tab_h;
+    int Nmax_all = 0;
+    for (auto &kv : s.coeffs) Nmax_all = std::max(Nmax_all, kv.first);
+    tab_off_h.assign(Nmax_all + 1, 0);
+    for (auto &kv : s.coeffs) {
+        tab_off_h[kv.first] = (int)tab_h.size();
+        tab_h.insert(tab_h.end(), kv.second.begin(), kv.second.end());
+    }
+    int rc;
+    if ((rc = dalloc_t(h, &h->tab, tab_h.size()))) return rc;
+    if ((rc = dalloc_t(h, &h->tab_off, tab_off_h.size()))) return rc;
+    if ((rc = upload(h, h->tab, tab_h.data(), tab_h.size()))) return rc;
+    if ((rc = upload(h, h->tab_off, tab_off_h.data(), tab_off_h.size()))) return rc;
+
+    // ---- row constants of apply_RST_scaling / get_rho_T_fluc (df.cpp:425-438, 474)
+    std::vector<double> rowc(7 * (size_t)Ny);
+    for (int j = 0; j < Ny; ++j) {
+        double b;
+        if (s.R11[j] < 1e-10) b = 0.0;
+        else b = s.R21[j] / std::sqrt(s.R11[j]);
+        rowc[j] = std::sqrt(s.R11[j]);
+        rowc[Ny + j] = b;
+        rowc[2 * Ny + j] = std::sqrt(s.R22[j] - b * b);
+        rowc[3 * Ny + j] = std::sqrt(s.R33[j]);
+        rowc[4 * Ny + j] = -0.5 * (1.4 - 1) * s.Ms[j] * s.Ms[j] / s.Us[j];
+        rowc[5 * Ny + j] = s.Ts[j];
+        rowc[6 * Ny + j] = s.rhos[j];
+    }
+    if ((rc = dalloc_t(h, &h->rowc, rowc.size()))) return rc;
+    if ((rc = upload(h, h->rowc, rowc.data(), rowc.size()))) return rc;
+
+    // ---- per-component buffers
+    const size_t n_loc = (size_t)Ny * h->Nz_loc;
+    for (int c = 0; c < 3; ++c) {
+        CompDev &d = h->c[c];
+        const ComponentSetup &F = s.comp[c];
+        if ((rc = dalloc_t(h, &d.ry, (size_t)(Ny + 2 * d.Nyp) * h->Pz))) return rc;
+        if ((rc = dalloc_t(h, &d.rz, (size_t)Ny * d.rz_pitch))) return rc;
+        if ((rc = dalloc_t(h, &d.filt_old, n_loc))) return rc;
+        if ((rc = dalloc_t(h, &d.fluc, n_loc))) return rc;
+        if ((rc = dalloc_t(h, &d.Ny_row, Ny))) return rc;
+        if ((rc = dalloc_t(h, &d.Nz_row, Ny))) return rc;
+        if ((rc = upload(h, d.Ny_row, F.Ny_row.data(), Ny))) return rc;
+        if ((rc = upload(h, d.Nz_row, F.Nz_row.data(), Ny))) return rc;
+        if (h->coeff_mode == DF_COEFF_PACKED) {
+            // strip-tap-major offsets, one block per (strip, row)
+            for (int dir = 0; dir < 2; ++dir) {
+                const std::vector<int> &Nr = dir ? F.Nz_row : F.Ny_row;
+                std::vector<long long> off((size_t)h->nstrips * Ny);
+                long long run = 0;
+                for (int st = 0; st < h->nstrips; ++st)
+                    for (int j = 0; j < Ny; ++j) {
+                        off[(size_t)st * Ny + j] = run;
+                        run += (long long)(2 * Nr[j] + 1) * kStrip;
+                    }
+                long long **doff = dir ? &d.bzoff : &d.byoff;
+                double **dB = dir ? &d.Bz : &d.By;
+                (dir ? d.bz_elems : d.by_elems) = run;
+                if ((rc = dalloc_t(h, doff, off.size()))) return rc;
+                if ((rc = upload(h, *doff, off.data(), off.size()))) return rc;
+                if ((rc = dalloc_t(h, dB, (size_t)run))) return rc;
+                HIP_OR(launch_expand_coeffs(*dB, *doff, dir ? d.Nz_row : d.Ny_row, h->tab, h->tab_off, Ny,
+                                            h->nstrips, h->Nz_loc, h->stream),
+                       DF_EHIP);
+            }
+        }
+    }
+    if ((rc = dalloc_t(h, &h->T, n_loc))) return rc;
+    if ((rc = dalloc_t(h, &h->rho, n_loc))) return rc;
+
+    for (int c = 0; c < 3; ++c) {
+        g.ry[c] = h->c[c].ry;
+        g.rz[c] = h->c[c].rz;
+        g.Nzp[c] = h->c[c].Nzp;
+        g.rz_pitch[c] = h->c[c].rz_pitch;
+    }
+    if ((rc = dalloc_t(h, &h->rstate, 2))) return rc;
+    if ((rc = dalloc_t(h, &h->counts, h->rng_blocks))) return rc;
+    if ((rc = dalloc_t(h, &h->offsets, h->rng_blocks))) return rc;
+    HIP_OR(hipHostMalloc((void **)&h->err_host, sizeof(int), hipHostMallocMapped), DF_EHIP);
+    *h->err_host = 0;
+    HIP_OR(hipHostGetDevicePointer((void **)&h->err_dev, h->err_host, 0), DF_EHIP);
+
+    uint64_t seed = cfg->seed;
+    if (cfg->seed_from_random_device) seed = (uint64_t)std::random_device{}(); // df.cpp:334
+    RngStateDev st0{pcg_seed1(seed), 0, 0, 0.0};
+    if (cfg->rng_resume) st0 = RngStateDev{cfg->rng_state, cfg->rng_saved_flag ? 1 : 0, 0, cfg->rng_saved};
+    if ((rc = upload(h, h->rstate, &st0, 1))) return rc;
+
+    // ---- halo buffers + communicator
+    if (h->world > 1) {
+        h->halo_elems = 0;
+        for (int c = 0; c < 3; ++c) h->halo_elems += (size_t)Ny * h->c[c].Nzp;
+        if ((rc = dalloc_t(h, &h->send_l, h->halo_elems))) return rc;
+        if ((rc = dalloc_t(h, &h->send_r, h->halo_elems))) return rc;
+        if ((rc = dalloc_t(h, &h->recv_l, h->halo_elems))) return rc;
+        if ((rc = dalloc_t(h, &h->recv_r, h->halo_elems))) return rc;
+        if (cfg->comm_id) {
+            ncclUniqueId id;
+            std::memcpy(&id, cfg->comm_id, sizeof(id));
+            NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
+        }
+    }
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+int step0(df_handle *h)
+{
+    // Constructor step 0 (df.cpp:57-62): noise, sweeps, RST; no correlation, no SRA.
+    int rc;
+    if ((rc = phase_rng(h))) return rc;
+    if ((rc = phase_ypass(h, 7))) return rc;
+    if ((rc = phase_halo_rccl(h))) return rc;
+    if ((rc = phase_zpass(h, false, false, 0.0))) return rc;
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return check_rng_error(h);
+}
+
+void destroy(df_handle *h)
+{
+    if (!h) return;
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &pe : h->ev)
+        for (auto &e : pe.e) (void)hipEventDestroy(e);
+    for (void *p : h->allocs) (void)hipFree(p);
+    if (h->err_host) (void)hipHostFree(h->err_host);
+    if (h->comm) ncclCommDestroy(h->comm);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+// Strips of one plane held by handles of this process: each phase runs on every
+// handle before the halo copies, then the z-pass. corr_sra = false is step 0.
+int group_step(df_handle **hs, int n, bool corr_sra, double dt)
+{
+    if (!hs || n < 1) return fail(DF_EINVAL, "empty handle group");
+    for (int r = 0; r < n; ++r) {
+        if (!hs[r]) return fail(DF_EINVAL, "null handle in group");
+        if (hs[r]->rank != r || hs[r]->world != n || hs[r]->comm)
+            return fail(DF_EINVAL, "group handles must be ranks 0..n-1 of one plane, created without comm_id");
+    }
+    int rc;
+    for (int r = 0; r < n; ++r) {
+        df_handle *h = hs[r];
+        HIP_OR(hipSetDevice(h->device), DF_EHIP);
+        if ((rc = check_rng_error(h))) return rc;
+        if ((rc = phase_rng(h))) return rc;
+        if ((rc = phase_ypass(h, 7))) return rc;
+        if ((rc = phase_halo_pack(h))) return rc;
+    }
+    for (int r = 0; r < n; ++r) HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
+    for (int r = 0; r < n; ++r) {
+        df_handle *h = hs[r];
+        HIP_OR(hipSetDevice(h->device), DF_EHIP);
+        const size_t bytes = h->halo_elems * sizeof(double);
+        if (r > 0) HIP_OR(hipMemcpyAsync(h->recv_l, hs[r - 1]->send_r, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
+        if (r < n - 1) HIP_OR(hipMemcpyAsync(h->recv_r, hs[r + 1]->send_l, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
+        if ((rc = phase_halo_unpack(h))) return rc;
+        if ((rc = phase_zpass(h, corr_sra, corr_sra, dt))) return rc;
+    }
+    for (int r = 0; r < n; ++r) {
+        HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
+        if ((rc = check_rng_error(hs[r]))) return rc;
+        if (corr_sra && (rc = write_csv_if(hs[r]))) return rc;
+    }
+    return DF_OK;
+}
+
+bool valid(df_handle *h)
+{
+    if (!h) {
+        g_err = "null handle";
+        return false;
+    }
+    return true;
+}
+
+// Handles that own GPU state (not host-only).
+bool valid_dev(df_handle *h)
+{
+    if (!valid(h)) return false;
+    if (h->device < 0) {
+        g_err = "host-only handle (created with device = -1) has no GPU state";
+        return false;
+    }
+    return true;
+}
+
+} // namespace
+
+// =================================================================== C ABI
+
+extern "C" {
+
+int df_abi_version(void) { return DF_ABI_VERSION; }
+
+const char *df_last_error(void) { return g_err.c_str(); }
+
+void df_config_default(df_config_c *cfg)
+{
+    std::memset(cfg, 0, sizeof(*cfg));
+    Flow f;
+    cfg->d_i = f.d_i;
+    cfg->rho_e = f.rho_e;
+    cfg->U_e = f.U_e;
+    cfg->mu_e = f.mu;
+    cfg->seed = 0;
+    cfg->seed_from_random_device = 1;
+    cfg->plane = DF_PLANE_NATIVE;
+    cfg->coeff_mode = DF_COEFF_PACKED;
+    cfg->world = 1;
+    cfg->rows_per_wave = 8;
+}
+
+df_handle *df_create(const df_config_c *cfg)
+{
+    if (!cfg) {
+        g_err = "null config";
+        return nullptr;
+    }
+    df_handle *h = new df_handle();
+    int rc = DF_OK;
+    if (cfg->device < 0 && cfg->world > 1 && !cfg->comm_id) rc = DF_OK; // host-only strip planning
+    else if (cfg->world > 1 && !cfg->comm_id)
+        rc = fail(DF_EINVAL, "world > 1 needs comm_id (RCCL) or df_create_group (in-process strips)");
+    if (rc == DF_OK) rc = build(h, cfg);
+    if (rc == DF_OK && h->device >= 0) rc = step0(h);
+    if (rc != DF_OK) {
+        std::string keep = g_err;
+        destroy(h);
+        g_err = keep;
+        return nullptr;
+    }
+    g_err.clear();
+    return h;
+}
+
+int df_filter(df_handle *h, double dt)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    int rc = check_rng_error(h);
+    if (rc) return rc;
+    if (h->world > 1 && !h->comm) return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    const bool prof = h->profiling && h->ev_used < h->ev.size();
+    ev_record(h, 0);
+    if ((rc = phase_rng(h))) return rc;
+    ev_record(h, 1);
+    if ((rc = phase_ypass(h, 7))) return rc;
+    ev_record(h, 2);
+    if ((rc = phase_halo_rccl(h))) return rc;
+    ev_record(h, 3);
+    if ((rc = phase_zpass(h, true, true, dt))) return rc;
+    ev_record(h, 4);
+    if (prof) h->ev_used++;
+    return write_csv_if(h);
+}
+
+int df_filter_group(df_handle **hs, int n, double dt) { return group_step(hs, n, true, dt); }
+
+int df_create_group(const df_config_c *cfgs, int n, df_handle **out)
+{
+    if (!cfgs || !out || n < 1) return fail(DF_EINVAL, "bad group arguments");
+    for (int r = 0; r < n; ++r) out[r] = nullptr;
+    int rc = DF_OK;
+    for (int r = 0; r < n && rc == DF_OK; ++r) {
+        if (cfgs[r].comm_id || cfgs[r].rank != r || cfgs[r].world != n) {
+            rc = fail(DF_EINVAL, "group configs must be ranks 0..n-1 of one plane without comm_id");
+            break;
+        }
+        out[r] = new df_handle();
+        rc = build(out[r], &cfgs[r]);
+    }
+    if (rc == DF_OK) rc = group_step(out, n, false, 0.0); // the constructor's step 0
+    if (rc != DF_OK) {
+        std::string keep = g_err;
+        for (int r = 0; r < n; ++r) {
+            destroy(out[r]);
+            out[r] = nullptr;
+        }
+        g_err = keep;
+    }
+    return rc;
+}
+
+int df_generate_white_noise(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    return phase_rng(h);
+}
+
+int df_filtering_sweeps(df_handle *h, int comp)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    if (comp < 0 || comp > 2) return fail(DF_EINVAL, "comp must be 0, 1 or 2");
+    if (h->world > 1) return fail(DF_EINVAL, "stage API is single-strip only");
+    int rc;
+    if (!h->c[comp].filt && (rc = dalloc_t(h, &h->c[comp].filt, (size_t)h->Ny * h->Nz_loc))) return rc;
+    if ((rc = phase_ypass(h, 1 << comp))) return rc;
+    SweepArgs a = sweep_args(h);
+    a.comps_mask = 1 << comp;
+    a.write_filt = 1;
+    HIP_OR(launch_zpass(a, h->coeff_mode == DF_COEFF_TABLE, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+static int stage_elementwise(df_handle *h, int op, int comp, double dt)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    for (int c = 0; c < 3; ++c)
+        if ((op == 1 || c == comp) && !h->c[c].filt && op != 2)
+            return fail(DF_EINVAL, "df_filtering_sweeps must run before this stage");
+    SweepArgs a = sweep_args(h);
+    if (op == 0) {
+        const double pi = 3.141592654; // df.cpp:411
+        const double alpha = std::exp(-pi * dt / h->setup.comp[comp].Lt);
+        a.sa[comp] = std::sqrt(alpha);
+        a.s1a[comp] = std::sqrt(1.0 - alpha);
+    }
+    HIP_OR(launch_stage(a, op, comp, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+int df_correlate_fields(df_handle *h, int comp, double dt)
+{
+    if (comp < 0 || comp > 2) return fail(DF_EINVAL, "comp must be 0, 1 or 2");
+    return stage_elementwise(h, 0, comp, dt);
+}
+
+int df_apply_RST_scaling(df_handle *h) { return stage_elementwise(h, 1, 0, 0.0); }
+
+int df_get_rho_T_fluc(df_handle *h) { return stage_elementwise(h, 2, 0, 0.0); }
+
+int df_get_field(df_handle *h, int which, double *out)
+{
+    if (!valid_dev(h) || !out) return DF_EINVAL;
+    const double *src = df_device_field(h, which);
+    if (!src) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipMemcpyAsync(out, src, (size_t)h->Ny * h->Nz_loc * 8, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return check_rng_error(h);
+}
+
+const double *df_device_field(df_handle *h, int which)
+{
+    if (!valid_dev(h)) return nullptr;
+    switch (which) {
+    case DF_U: case DF_V: case DF_W: return h->c[which].fluc;
+    case DF_T: return h->T;
+    case DF_RHO: return h->rho;
+    case DF_FILT_OLD_U: case DF_FILT_OLD_V: case DF_FILT_OLD_W: return h->c[which - DF_FILT_OLD_U].filt_old;
+    }
+    g_err = "unknown field";
+    return nullptr;
+}
+
+int df_dims(df_handle *h, int *Ny, int *Nz, int *z0, int *z1)
+{
+    if (!valid(h)) return DF_EINVAL;
+    if (Ny) *Ny = h->Ny;
+    if (Nz) *Nz = h->Nz_g;
+    if (z0) *z0 = h->z0;
+    if (z1) *z1 = h->z1;
+    return DF_OK;
+}
+
+int df_get_row(df_handle *h, int which, double *out)
+{
+    if (!valid(h) || !out) return DF_EINVAL;
+    const Setup &s = h->setup;
+    const std::vector<double> *v = nullptr;
+    switch (which) {
+    case DF_ROW_R11: v = &s.R11; break;
+    case DF_ROW_R21: v = &s.R21; break;
+    case DF_ROW_R22: v = &s.R22; break;
+    case DF_ROW_R33: v = &s.R33; break;
+    case DF_ROW_US: v = &s.Us; break;
+    case DF_ROW_TS: v = &s.Ts; break;
+    case DF_ROW_RHOS: v = &s.rhos; break;
+    case DF_ROW_MS: v = &s.Ms; break;
+    case DF_ROW_PS: v = &s.Ps; break;
+    case DF_ROW_YC: v = &s.yc; break;
+    case DF_ROW_YC_D: v = &s.yc_d; break;
+    default: return fail(DF_EINVAL, "unknown row");
+    }
+    std::copy(v->begin(), v->begin() + s.Ny, out);
+    return DF_OK;
+}
+
+double df_get_scalar(df_handle *h, int which)
+{
+    if (!valid(h)) return NAN;
+    switch (which) {
+    case 0: return h->setup.u_tau;
+    case 1: return h->setup.tau_w;
+    case 2: return h->setup.d_v;
+    }
+    return NAN;
+}
+
+int df_get_halfwidths(df_handle *h, int comp, int dir, int *out)
+{
+    if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
+    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    for (int j = 0; j < h->Ny; ++j)
+        for (int k = 0; k < h->Nz_loc; ++k) out[(size_t)j * h->Nz_loc + k] = Nr[j];
+    return DF_OK;
+}
+
+int df_get_offsets(df_handle *h, int comp, int dir, int *out)
+{
+    if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
+    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    long long b_size = 0; // df.cpp:151-152 / 191-192, over this strip's cells in row-major order
+    for (int j = 0; j < h->Ny; ++j)
+        for (int k = 0; k < h->Nz_loc; ++k) {
+            b_size += 2 * Nr[j] + 1;
+            out[(size_t)j * h->Nz_loc + k] = (int)(b_size - Nr[j] - 1);
+        }
+    return DF_OK;
+}
+
+int df_get_comp_info(df_handle *h, int comp, int *Ny_max, int *Nz_max, long long *by_size, long long *bz_size)
+{
+    if (!valid(h) || comp < 0 || comp > 2) return fail(DF_EINVAL, "bad argument");
+    if (Ny_max) *Ny_max = h->c[comp].Nyp;
+    if (Nz_max) *Nz_max = h->c[comp].Nzp;
+    if (by_size) *by_size = h->c[comp].by_size;
+    if (bz_size) *bz_size = h->c[comp].bz_size;
+    return DF_OK;
+}
+
+int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n)
+{
+    if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
+    const long long need = dir ? h->c[comp].bz_size : h->c[comp].by_size;
+    if (n < need) return fail(DF_EINVAL, "output too small for the packed coefficient vector");
+    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    long long pos = 0;
+    for (int j = 0; j < h->Ny; ++j) {
+        const std::vector<double> &half = h->setup.coeffs.at(Nr[j]);
+        const int N = Nr[j];
+        for (int k = 0; k < h->Nz_loc; ++k)
+            for (int i = -N; i <= N; ++i) out[pos++] = half[i < 0 ? -i : i];
+    }
+    return DF_OK;
+}
+
+int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    RngStateDev st;
+    HIP_OR(hipMemcpyAsync(&st, h->rstate + (h->calls & 1), sizeof st, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    if (state) *state = st.state;
+    if (saved_flag) *saved_flag = st.saved_flag;
+    if (saved) *saved = st.saved;
+    return check_rng_error(h);
+}
+
+int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    RngStateDev st{state, saved_flag ? 1 : 0, 0, saved};
+    HIP_OR(hipMemcpyAsync(h->rstate + (h->calls & 1), &st, sizeof st, hipMemcpyHostToDevice, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+long long df_stream_length(df_handle *h) { return valid(h) ? (long long)h->geom.Q : -1; }
+
+int df_set_profiling(df_handle *h, int on)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    if (on && h->ev.empty()) {
+        h->ev.resize(1024);
+        for (auto &pe : h->ev)
+            for (auto &e : pe.e) HIP_OR(hipEventCreate(&e), DF_EHIP);
+    }
+    int rc = drain_profile(h);
+    h->profiling = on != 0;
+    h->prof = df_profile{};
+    return rc;
+}
+
+int df_get_profile(df_handle *h, df_profile *out)
+{
+    if (!valid_dev(h) || !out) return DF_EINVAL;
+    int rc = drain_profile(h);
+    *out = h->prof;
+    return rc;
+}
+
+int df_sync(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return check_rng_error(h);
+}
+
+void *df_stream(df_handle *h) { return valid_dev(h) ? (void *)h->stream : nullptr; }
+
+int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n)
+{
+    if (!valid_dev(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
+    const CompDev &d = h->c[comp];
+    const int width = dir ? h->Nz_loc + 2 * d.Nzp : h->Nz_loc;
+    const int rows = dir ? h->Ny : h->Ny + 2 * d.Nyp;
+    if (n < (long long)width * rows) return fail(DF_EINVAL, "output too small");
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipMemcpy2DAsync(out, (size_t)width * 8, dir ? d.rz : d.ry, (size_t)(dir ? d.rz_pitch : h->Pz) * 8,
+                            (size_t)width * 8, rows, hipMemcpyDeviceToHost, h->stream),
+           DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+double df_algorithmic_bytes(df_handle *h, int kernel)
+{
+    // SURVEY 8d byte model: per component 8(|by|+|bz|) + 16n (N_ys, N_zs, by/bz offsets)
+    // + 24n (filt_old read + write, fluc write); + 16n for T', rho'. The y-pass gets
+    // 8|by| + 8n, the z-pass + epilogue the rest.
+    if (!valid(h)) return -1.0;
+    const double n = (double)h->Ny * h->Nz_loc;
+    double y = 0, z = 0;
+    for (int c = 0; c < 3; ++c) {
+        y += 8.0 * h->c[c].by_size + 8.0 * n;
+        z += 8.0 * h->c[c].bz_size + 8.0 * n + 24.0 * n;
+    }
+    z += 16.0 * n;
+    return kernel == 0 ? y : kernel == 1 ? z : y + z;
+}
+
+int df_comm_unique_id(void *out, size_t len)
+{
+    if (!out || len < sizeof(ncclUniqueId)) return fail(DF_EINVAL, "need 128 bytes for the RCCL unique id");
+    ncclUniqueId id;
+    NCCL_OR(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, sizeof id);
+    return DF_OK;
+}
+
+void df_destroy(df_handle *h) { destroy(h); }
+
+} // extern "C"

@@ -1,0 +1,535 @@
+// HIP kernels (gfx950 / CDNA4) for DIGITAL_FILTER::filter(dt)
+// (reference: digital-filtering-c++/df/df.cpp:332-485).
+//
+//   K0 expand_coeffs   per-N coefficient table -> strip-tap-major By/Bz   (setup)
+//   K1 rng_count       pcg32 + polar accept flags, per-block accept counts
+//   K2 rng_scan        exclusive scan of block counts (global accept ranks)
+//   K3 rng_generate    normals in the reference's stream order -> ry, rz halo
+//   K4 ypass           y-convolution (df.cpp:359-383), R rows per wave in registers
+//   K5 zpass_epilogue  z-convolution (df.cpp:385-405) fused with correlate
+//                      (408-417), RST scaling (419-447) and SRA T'/rho' (470-485)
+//   K6 halo pack/unpack  z-halo columns for the multi-GPU strip exchange
+//
+// All FP64 and built with -ffp-contract=off: every product and sum rounds on its
+// own, in the reference's order, so the sweeps are bit-exact given equal noise.
+#include "df_kernels.hpp"
+#include "df_rng.hpp"
+
+namespace dfamd {
+
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ------------------------------------------------------------------ K0 setup
+
+__global__ __launch_bounds__(256) void expand_coeffs_kernel(double *__restrict__ B,
+                                                            const long long *__restrict__ off,
+                                                            const int *__restrict__ N_row,
+                                                            const double *__restrict__ tab,
+                                                            const int *__restrict__ tab_off, int Ny,
+                                                            int Nz_loc)
+{
+    const int sj = blockIdx.x; // s * Ny + j
+    const int s = sj / Ny, j = sj - s * Ny;
+    const int N = N_row[j];
+    const double *h = tab + tab_off[N];
+    double *dst = B + off[sj];
+    const int total = (2 * N + 1) * kStrip;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int t = e / kStrip, cell = e - t * kStrip;
+        const int i = t - N, ai = i < 0 ? -i : i;
+        dst[e] = (s * kStrip + cell < Nz_loc) ? h[ai] : 0.0;
+    }
+}
+
+hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_row, const double *tab,
+                                const int *tab_off, int Ny, int nstrips, int Nz_loc, hipStream_t st)
+{
+    hipLaunchKernelGGL(expand_coeffs_kernel, dim3((unsigned)nstrips * Ny), dim3(256), 0, st, B, off, N_row,
+                       tab, tab_off, Ny, Nz_loc);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- K1-K3 RNG
+//
+// Attempt t (0-based within the call) consumes pcg32 outputs 4t..4t+3 of the
+// stream that starts at the call's state S. Block b owns attempts
+// [b*4096, (b+1)*4096); thread `tid` handles b*4096 + m*256 + tid, m = 0..15,
+// so consecutive lanes hold consecutive attempts and a wave's accepted attempts
+// map to consecutive stream positions (coalesced stores).
+
+__device__ __forceinline__ uint64_t thread_first_state(uint64_t S, int b, int tid)
+{
+    return pcg_advance(S, 4ull * ((uint64_t)b * kRngBlockAttempts + (uint64_t)tid));
+}
+
+__global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                               int *__restrict__ counts)
+{
+    __shared__ int wsum[kRngThreads / 64];
+    const int tid = threadIdx.x;
+    uint64_t st = thread_first_state(sin->state, blockIdx.x, tid);
+    int cnt = 0;
+#pragma unroll 4
+    for (int m = 0; m < kRngPerThread; ++m) {
+        PolarAttempt a = polar_attempt(st);
+        cnt += a.accept ? 1 : 0;
+        st = g.hop_mult * st + g.hop_plus;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((tid & 63) == 0) wsum[tid >> 6] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+        int t = 0;
+        for (int w = 0; w < kRngThreads / 64; ++w) t += wsum[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(1024) void rng_scan_kernel(const int *__restrict__ counts,
+                                                       long long *__restrict__ offsets, int nblocks,
+                                                       const RngStateDev *__restrict__ sin, uint64_t Q,
+                                                       int *__restrict__ err)
+{
+    __shared__ long long part[1024];
+    const int tid = threadIdx.x;
+    const int chunk = (nblocks + 1023) / 1024;
+    const int b0 = min(tid * chunk, nblocks), b1 = min(b0 + chunk, nblocks);
+    long long s = 0;
+    for (int b = b0; b < b1; ++b) s += counts[b];
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        long long v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    long long base = tid ? part[tid - 1] : 0;
+    for (int b = b0; b < b1; ++b) {
+        offsets[b] = base;
+        base += counts[b];
+    }
+    if (tid == 1023) {
+        const uint64_t f = (uint64_t)sin->saved_flag;
+        const long long A = (long long)((Q - f + 1) / 2);
+        if (part[1023] < A) *err = 1; // not enough attempts launched: host re-sizes
+    }
+}
+
+// Stream position q -> destination in this GPU's buffers, or nullptr if the
+// reference draws that normal but this GPU never reads it (the r_zs interior,
+// df.cpp:377 overwrites it; columns owned by other GPUs).
+__device__ __forceinline__ double *stream_dest(const RngGeom &g, uint64_t q)
+{
+    int sidx = 0;
+#pragma unroll
+    for (int s = 1; s < 6; ++s) sidx += (q >= g.seg[s]) ? 1 : 0;
+    const uint32_t p = (uint32_t)(q - g.seg[sidx]);
+    const int c = sidx >> 1;
+    if ((sidx & 1) == 0) { // r_ys: Nz_g columns per row
+        const uint32_t row = p / (uint32_t)g.Nz_g;
+        const int col = (int)(p - row * (uint32_t)g.Nz_g);
+        if (col < g.z0 || col >= g.z1) return nullptr;
+        return g.ry[c] + (size_t)row * g.Pz + (col - g.z0);
+    }
+    const uint32_t W = (uint32_t)(g.Nz_g + 2 * g.Nzp[c]);
+    const uint32_t row = p / W;
+    const int gc = (int)(p - row * W);
+    int lc;
+    if (gc < g.Nzp[c]) {
+        if (!g.is_first) return nullptr;
+        lc = gc;
+    } else if (gc >= g.Nzp[c] + g.Nz_g) {
+        if (!g.is_last) return nullptr;
+        lc = gc - g.z0;
+    } else {
+        return nullptr;
+    }
+    return g.rz[c] + (size_t)row * g.rz_pitch[c] + lc;
+}
+
+__global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                  RngStateDev *__restrict__ sout,
+                                                                  const long long *__restrict__ offsets)
+{
+    __shared__ int cnt[kRngPerThread][kRngThreads / 64];
+    __shared__ int pre[kRngPerThread][kRngThreads / 64];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    const long long Ob = offsets[blockIdx.x];
+    if (Ob >= A) return;
+
+    if (blockIdx.x == 0 && tid == 0 && f) {
+        double *d = stream_dest(g, 0);
+        if (d) *d = sin->saved * 1.0 + 0.0;
+    }
+    const uint64_t st0 = thread_first_state(sin->state, blockIdx.x, tid);
+    uint64_t st = st0;
+    for (int m = 0; m < kRngPerThread; ++m) {
+        PolarAttempt a = polar_attempt(st);
+        const uint64_t mask = __ballot(a.accept);
+        if (lane == 0) cnt[m][w] = __popcll(mask);
+        st = g.hop_mult * st + g.hop_plus;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int run = 0;
+        for (int m = 0; m < kRngPerThread; ++m)
+            for (int ww = 0; ww < kRngThreads / 64; ++ww) {
+                pre[m][ww] = run;
+                run += cnt[m][ww];
+            }
+    }
+    __syncthreads();
+    st = st0;
+    for (int m = 0; m < kRngPerThread; ++m) {
+        PolarAttempt a = polar_attempt(st);
+        const uint64_t mask = __ballot(a.accept);
+        if (a.accept) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            const long long rank = Ob + pre[m][w] + below;
+            if (rank < A) {
+                const uint64_t q0 = f + 2ull * (uint64_t)rank;
+                double *d0 = stream_dest(g, q0);
+                double *d1 = (q0 + 1 < g.Q) ? stream_dest(g, q0 + 1) : nullptr;
+                const bool last = (rank == A - 1);
+                if (d0 || d1 || last) {
+                    const double mult = sqrt(-2 * log(a.r2) / a.r2);
+                    const double xm = a.x * mult;
+                    const double ym = a.y * mult;
+                    if (d0) *d0 = ym * 1.0 + 0.0;
+                    if (d1) *d1 = xm * 1.0 + 0.0;
+                    if (last) {
+                        sout->state = st; // state after this attempt's 4th output
+                        sout->saved_flag = (int)((g.Q - f) & 1u);
+                        sout->saved = xm;
+                    }
+                }
+            }
+        }
+        st = g.hop_mult * st + g.hop_plus;
+    }
+}
+
+hipError_t launch_rng(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
+                      long long *offsets, int *err, int nblocks, hipStream_t st)
+{
+    hipLaunchKernelGGL(rng_count_kernel, dim3(nblocks), dim3(kRngThreads), 0, st, g, st_in, counts);
+    hipLaunchKernelGGL(rng_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, nblocks, st_in, g.Q, err);
+    hipLaunchKernelGGL(rng_generate_kernel, dim3(nblocks), dim3(kRngThreads), 0, st, g, st_in, st_out, offsets);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- K4 y-pass
+//
+// One wave = one tile of R consecutive rows x one 128-cell strip; lane l owns
+// cells 2l, 2l+1. Walking the noise rows t once, each noise row is loaded a
+// single time and applied to every tile row r whose stencil covers it (tap
+// i = t - r), so per cell the taps still accumulate in the reference's order
+// i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
+// coalesced dwordx4 per (row, tap).
+
+template <int R, bool TABLE>
+__global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
+{
+    const int c = blockIdx.y;
+    if (!((a.comps_mask >> c) & 1)) return;
+    const int lane = threadIdx.x & 63;
+    const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (tile >= a.nstrips * nrowblk) return;
+    const int s = tile / nrowblk;          // strip-major: neighbouring tiles share noise rows
+    const int j0 = (tile - s * nrowblk) * R;
+    const int Ny = a.Ny;
+    const int nr = min(R, Ny - j0);
+    const int col = s * kStrip + 2 * lane;
+    const int Pz = a.Pz;
+
+    int N[R];
+    const double *bp[R];
+    const double *tb[R];
+    int Nlo = 1 << 30, Nhi = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        N[r] = 0;
+        bp[r] = nullptr;
+        tb[r] = nullptr;
+        if (r < nr) {
+            N[r] = a.Ny_row[c][j0 + r];
+            Nlo = min(Nlo, N[r]);
+            Nhi = max(Nhi, N[r]);
+            if (TABLE) tb[r] = a.tab + a.tab_off[N[r]];
+            else bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + r] + (ptrdiff_t)(N[r] - r) * kStrip + 2 * lane;
+        }
+    }
+    const double *np = a.ry[c] + (size_t)(j0 + a.Nyp[c]) * Pz + col;
+
+    double acc0[R], acc1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0.0;
+
+    auto coef = [&](int r, int t) -> double2 {
+        if (TABLE) {
+            const int i = t - r;
+            const double b = tb[r][i < 0 ? -i : i];
+            return make_double2(b, b);
+        }
+        return *reinterpret_cast<const double2 *>(bp[r] + (ptrdiff_t)t * kStrip);
+    };
+    auto predicated = [&](int t) {
+        const double2 n = *reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = t - r;
+            if (r < nr && i >= -N[r] && i <= N[r]) {
+                const double2 b = coef(r, t);
+                acc0[r] += b.x * n.x;
+                acc1[r] += b.y * n.y;
+            }
+        }
+    };
+    auto body = [&](int t) {
+        const double2 n = *reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz);
+        double2 b[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) b[r] = coef(r, t);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc0[r] += b[r].x * n.x;
+            acc1[r] += b[r].y * n.y;
+        }
+    };
+
+    const int tlo = -Nhi, thi = (nr - 1) + Nhi;
+    const bool body_ok = (nr == R) && (R - 1 - Nlo <= Nlo);
+    const int bl = body_ok ? R - 1 - Nlo : thi + 1;
+    const int bh = body_ok ? Nlo : thi;
+    int t = tlo;
+    for (; t < bl; ++t) predicated(t);
+    for (; t + 1 <= bh; t += 2) {
+        body(t);
+        body(t + 1);
+    }
+    for (; t <= bh; ++t) body(t);
+    for (; t <= thi; ++t) predicated(t);
+
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r < nr) {
+            double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + col;
+            if (col + 1 < a.Nz_loc) *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
+            else if (col < a.Nz_loc) o[0] = acc0[r];
+        }
+    }
+}
+
+template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
+{
+    const int nrowblk = (a.Ny + R - 1) / R;
+    const long long tiles = (long long)a.nstrips * nrowblk;
+    const unsigned blocks = (unsigned)((tiles + 3) / 4);
+    hipLaunchKernelGGL((ypass_kernel<R, TABLE>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    return hipGetLastError();
+}
+
+hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
+{
+    switch (rows_per_wave) {
+    case 1: return table ? launch_ypass_t<1, true>(a, st) : launch_ypass_t<1, false>(a, st);
+    case 2: return table ? launch_ypass_t<2, true>(a, st) : launch_ypass_t<2, false>(a, st);
+    case 4: return table ? launch_ypass_t<4, true>(a, st) : launch_ypass_t<4, false>(a, st);
+    default: return table ? launch_ypass_t<8, true>(a, st) : launch_ypass_t<8, false>(a, st);
+    }
+}
+
+// ------------------------------------------------------ K5 z-pass + epilogue
+
+template <bool TABLE>
+__global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int Ny = a.Ny;
+    if (tile >= a.nstrips * Ny) return;
+    const int j = tile / a.nstrips;
+    const int s = tile - j * a.nstrips;
+    const int col = s * kStrip + 2 * lane;
+
+    double f0[3], f1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        f0[c] = f1[c] = 0.0;
+        if (!((a.comps_mask >> c) & 1)) continue;
+        const int N = a.Nz_row[c][j];
+        const double *x = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col;
+        const double *bp = TABLE ? nullptr
+                                 : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + (ptrdiff_t)N * kStrip + 2 * lane;
+        const double *tb = TABLE ? a.tab + a.tab_off[N] : nullptr;
+        double acc0 = 0.0, acc1 = 0.0;
+        int i = -N;
+        for (; i + 3 <= N; i += 4) {
+            double2 b[4];
+            double x0[4], x1[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (TABLE) {
+                    const int ii = i + u;
+                    const double v = tb[ii < 0 ? -ii : ii];
+                    b[u] = make_double2(v, v);
+                } else {
+                    b[u] = *reinterpret_cast<const double2 *>(bp + (ptrdiff_t)(i + u) * kStrip);
+                }
+                x0[u] = x[i + u];
+                x1[u] = x[i + u + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                acc0 += b[u].x * x0[u];
+                acc1 += b[u].y * x1[u];
+            }
+        }
+        for (; i <= N; ++i) {
+            double2 b;
+            if (TABLE) {
+                const double v = tb[i < 0 ? -i : i];
+                b = make_double2(v, v);
+            } else {
+                b = *reinterpret_cast<const double2 *>(bp + (ptrdiff_t)i * kStrip);
+            }
+            acc0 += b.x * x[i];
+            acc1 += b.y * x[i + 1];
+        }
+        f0[c] = acc0;
+        f1[c] = acc1;
+    }
+
+    if (a.write_filt) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (!((a.comps_mask >> c) & 1)) continue;
+            const size_t idx = (size_t)j * a.Nz_loc + col;
+            if (col < a.Nz_loc) a.filt[c][idx] = f0[c];
+            if (col + 1 < a.Nz_loc) a.filt[c][idx + 1] = f1[c];
+        }
+        return;
+    }
+    const double *rc = a.rowc;
+    const double sR11 = rc[j], bb = rc[Ny + j], sR22b = rc[2 * Ny + j], sR33 = rc[3 * Ny + j];
+    const double t1 = rc[4 * Ny + j], Ts = rc[5 * Ny + j], rh = rc[6 * Ny + j];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int k = col + e;
+        if (k >= a.Nz_loc) continue;
+        const size_t idx = (size_t)j * a.Nz_loc + k;
+        double fu = e ? f1[0] : f0[0], fv = e ? f1[1] : f0[1], fw = e ? f1[2] : f0[2];
+        if (a.do_corr) { // df.cpp:415
+            fu = a.filt_old[0][idx] * a.sa[0] + fu * a.s1a[0];
+            fv = a.filt_old[1][idx] * a.sa[1] + fv * a.s1a[1];
+            fw = a.filt_old[2][idx] * a.sa[2] + fw * a.s1a[2];
+        }
+        const double up = sR11 * fu;             // df.cpp:436
+        const double vp = bb * fu + sR22b * fv;  // df.cpp:437
+        const double wp = sR33 * fw;             // df.cpp:438
+        a.fluc[0][idx] = up;
+        a.fluc[1][idx] = vp;
+        a.fluc[2][idx] = wp;
+        a.filt_old[0][idx] = fu; // df.cpp:440-442
+        a.filt_old[1][idx] = fv;
+        a.filt_old[2][idx] = fw;
+        if (a.do_sra) { // df.cpp:474-481
+            const double t2 = t1 * up;
+            a.T[idx] = t2 * Ts;
+            a.rho[idx] = -t2 * rh;
+        }
+    }
+}
+
+hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
+{
+    const long long tiles = (long long)a.nstrips * a.Ny;
+    const unsigned blocks = (unsigned)((tiles + 3) / 4);
+    if (table) hipLaunchKernelGGL(zpass_kernel<true>, dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(zpass_kernel<false>, dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------- stage API elementwise ops
+
+__global__ void stage_kernel(SweepArgs a, int op, int comp)
+{
+    const size_t n = (size_t)a.Ny * a.Nz_loc;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
+        const int j = (int)(idx / a.Nz_loc);
+        const double *rc = a.rowc;
+        if (op == 0) {
+            a.filt[comp][idx] = a.filt_old[comp][idx] * a.sa[comp] + a.filt[comp][idx] * a.s1a[comp];
+        } else if (op == 1) {
+            const double fu = a.filt[0][idx], fv = a.filt[1][idx], fw = a.filt[2][idx];
+            a.fluc[0][idx] = rc[j] * fu;
+            a.fluc[1][idx] = rc[a.Ny + j] * fu + rc[2 * a.Ny + j] * fv;
+            a.fluc[2][idx] = rc[3 * a.Ny + j] * fw;
+            a.filt_old[0][idx] = fu;
+            a.filt_old[1][idx] = fv;
+            a.filt_old[2][idx] = fw;
+        } else {
+            const double t2 = rc[4 * a.Ny + j] * a.fluc[0][idx];
+            a.T[idx] = t2 * rc[5 * a.Ny + j];
+            a.rho[idx] = -t2 * rc[6 * a.Ny + j];
+        }
+    }
+}
+
+hipError_t launch_stage(const SweepArgs &a, int op, int comp, hipStream_t st)
+{
+    hipLaunchKernelGGL(stage_kernel, dim3(1024), dim3(256), 0, st, a, op, comp);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ K6 z-halo
+
+__global__ void halo_pack_kernel(SweepArgs a, double *__restrict__ sl, double *__restrict__ sr)
+{
+    size_t base = 0;
+    for (int c = 0; c < 3; ++c) {
+        const int W = a.Nzp[c];
+        const size_t n = (size_t)a.Ny * W;
+        for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+            const int j = (int)(e / W), kk = (int)(e - (size_t)j * W);
+            const double *row = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c];
+            if (sl) sl[base + e] = row[kk];
+            if (sr) sr[base + e] = row[a.Nz_loc - W + kk];
+        }
+        base += n;
+    }
+}
+
+__global__ void halo_unpack_kernel(SweepArgs a, const double *__restrict__ rl, const double *__restrict__ rr)
+{
+    size_t base = 0;
+    for (int c = 0; c < 3; ++c) {
+        const int W = a.Nzp[c];
+        const size_t n = (size_t)a.Ny * W;
+        for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+            const int j = (int)(e / W), kk = (int)(e - (size_t)j * W);
+            double *row = a.rz[c] + (size_t)j * a.rz_pitch[c];
+            if (rl) row[kk] = rl[base + e];
+            if (rr) row[a.Nzp[c] + a.Nz_loc + kk] = rr[base + e];
+        }
+        base += n;
+    }
+}
+
+hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st)
+{
+    hipLaunchKernelGGL(halo_pack_kernel, dim3(512), dim3(256), 0, st, a, send_l, send_r);
+    return hipGetLastError();
+}
+
+hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st)
+{
+    hipLaunchKernelGGL(halo_unpack_kernel, dim3(512), dim3(256), 0, st, a, recv_l, recv_r);
+    return hipGetLastError();
+}
+
+} // namespace dfamd

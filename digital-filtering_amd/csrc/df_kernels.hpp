@@ -1,0 +1,77 @@
+// Device-side data contract and kernel launchers for the filter(dt) hot path.
+//
+// HBM layout (one handle = one GPU = one z-strip [z0, z1) of the plane):
+//   ry[c]   noise for the y-pass, (Ny + 2*Nyp_c) rows x Pz columns, Pz = 128*nstrips
+//           (reference r_ys, df.cpp:197, row stride padded from Nz to Pz).
+//   rz[c]   Ny rows x rz_pitch_c, rz_pitch_c = Pz + 2*Nzp_c; local column Nzp_c + k
+//           holds y-filtered cell k (reference r_zs interior, df.cpp:377); columns
+//           [0,Nzp_c) and [Nzp_c+Nz_loc, ...) are the z-halo: raw noise at the
+//           global plane edges (df.cpp:343-348 quirk) or the neighbour's y-filtered
+//           columns when the plane is split over GPUs.
+//   By/Bz   filter coefficients in "strip-tap-major" order: for strip s (128 cells
+//           of one row) and row j, (2*N_sj+1) taps x 128 cells, cell fastest. The
+//           values are the reference's offset-packed by/bz (df.cpp:151-216), moved
+//           so that a wave reads tap i of 128 neighbouring cells as one 1 KiB load.
+//   filt_old[c], fluc[c], T, rho: dense Ny x Nz_loc, row-major idx = j*Nz_loc + k
+//           (reference FilterField::filt_old/fluc, df.hpp:24-34).
+#pragma once
+#include <cstdint>
+#include <hip/hip_runtime.h>
+
+namespace dfamd {
+
+constexpr int kStrip = 128;           // cells per strip (one wave, 2 per lane)
+constexpr int kRngThreads = 256;      // threads per RNG block
+constexpr int kRngPerThread = 16;     // polar attempts per thread
+constexpr int kRngBlockAttempts = kRngThreads * kRngPerThread;
+
+struct RngStateDev {
+    uint64_t state;
+    int saved_flag;
+    int pad;
+    double saved;
+};
+
+struct RngGeom {
+    uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
+    uint64_t Q;             // normals drawn per call
+    uint64_t hop_mult, hop_plus; // jump over (kRngThreads-1)*4 outputs
+    int Nz_g, Pz, z0, z1, is_first, is_last;
+    int Nzp[3], rz_pitch[3];
+    double *ry[3], *rz[3];
+};
+
+struct SweepArgs {
+    // y-pass
+    const double *ry[3];
+    double *rz[3];
+    const double *By[3], *Bz[3];
+    const long long *byoff[3], *bzoff[3]; // [s*Ny + j] element offsets
+    const int *Ny_row[3], *Nz_row[3];     // half-width per row
+    int Nyp[3], Nzp[3], rz_pitch[3];
+    int Ny, Nz_loc, Pz, nstrips;
+    // coefficient table (DF_COEFF_TABLE mode): half-vector of N at tab + tab_off[N]
+    const double *tab;
+    const int *tab_off;
+    // z-pass epilogue
+    double *filt_old[3], *fluc[3], *filt[3], *T, *rho;
+    const double *rowc;     // 7 x Ny: sqrt(R11), b, sqrt(R22-b^2), sqrt(R33), SRA t1, Ts, rhos
+    double sa[3], s1a[3];   // sqrt(alpha), sqrt(1-alpha) per component
+    int do_corr, do_sra, comps_mask;
+    int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
+};
+
+// Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.
+hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_row, const double *tab,
+                                const int *tab_off, int Ny, int nstrips, int Nz_loc, hipStream_t st);
+hipError_t launch_rng(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
+                      long long *offsets, int *err, int nblocks, hipStream_t st);
+hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st);
+hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
+// Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),
+// op 1 apply_RST_scaling (419-447), op 2 get_rho_T_fluc (470-485).
+hipError_t launch_stage(const SweepArgs &a, int op, int comp, hipStream_t st);
+hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st);
+hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st);
+
+} // namespace dfamd

@@ -1,0 +1,98 @@
+// pcg32 + libstdc++-11 polar-normal arithmetic shared by host setup and the HIP
+// kernels. This restates (does not include) the reference's third-party RNG:
+//   - pcg32 = setseq_xsh_rr_64_32 (pcg-cpp/include/pcg_random.hpp:1866), output
+//     from the OLD state (output_previous, :413-437), XSH-RR (:845-872),
+//     1-arg seeding state = (seed + inc)*mult + inc (:484-487), Brown jump (:639-662);
+//   - generate_canonical<double,53> (random.tcc:3346-3378): lo + hi*2^32, /2^64,
+//     clamp to nextafter(1,0);
+//   - normal_distribution<double>::operator() polar method (random.tcc:1800-1835):
+//     x then y from one attempt of 4 draws, accept 0 < x*x+y*y <= 1, emit y*m
+//     first and cache x*m; ret*1.0 + 0.0 maps -0.0 to +0.0.
+// Every floating-point line is written so that no FMA can be formed (the library
+// is compiled with -ffp-contract=off), matching the reference's x86-64 -O2 code.
+#pragma once
+#include <cstdint>
+
+#ifdef __HIPCC__
+#define DF_HD __host__ __device__ __forceinline__
+#else
+#define DF_HD inline
+#endif
+
+namespace dfamd {
+
+constexpr uint64_t kPcgMult = 6364136223846793005ULL;
+constexpr uint64_t kPcgInc = 1442695040888963407ULL;
+
+DF_HD uint32_t pcg_output(uint64_t s)
+{
+    uint32_t rot = (uint32_t)(s >> 59);
+    s ^= s >> 18;
+    uint32_t x = (uint32_t)(s >> 27);
+    return (x >> rot) | (x << ((32u - rot) & 31u));
+}
+
+DF_HD uint64_t pcg_seed1(uint64_t seed) { return (seed + kPcgInc) * kPcgMult + kPcgInc; }
+
+// Affine jump state -> mult*state + plus that equals `delta` single steps.
+struct PcgJump {
+    uint64_t mult, plus;
+};
+
+DF_HD PcgJump pcg_jump(uint64_t delta)
+{
+    uint64_t cur_mult = kPcgMult, cur_plus = kPcgInc, acc_mult = 1, acc_plus = 0;
+    while (delta > 0) {
+        if (delta & 1u) {
+            acc_mult *= cur_mult;
+            acc_plus = acc_plus * cur_mult + cur_plus;
+        }
+        cur_plus = (cur_mult + 1) * cur_plus;
+        cur_mult *= cur_mult;
+        delta >>= 1;
+    }
+    return {acc_mult, acc_plus};
+}
+
+DF_HD uint64_t pcg_advance(uint64_t state, uint64_t delta)
+{
+    PcgJump j = pcg_jump(delta);
+    return j.mult * state + j.plus;
+}
+
+// One polar attempt: consumes exactly 4 outputs starting at `state`.
+struct PolarAttempt {
+    double x, y, r2;
+    bool accept;
+};
+
+DF_HD double canonical_from(uint32_t lo, uint32_t hi)
+{
+    double sum = 0.0;
+    sum += (double)lo * 1.0;
+    sum += (double)hi * 4294967296.0;
+    double ret = sum / 18446744073709551616.0;
+    // nextafter(1.0, 0.0) == 1 - 2^-53
+    if (ret >= 1.0) ret = 0.99999999999999988897769753748434595763683319091796875;
+    return ret;
+}
+
+DF_HD PolarAttempt polar_attempt(uint64_t &state)
+{
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[i] = pcg_output(state);
+        state = state * kPcgMult + kPcgInc;
+    }
+    PolarAttempt a;
+    a.x = 2.0 * canonical_from(o[0], o[1]) - 1.0;
+    a.y = 2.0 * canonical_from(o[2], o[3]) - 1.0;
+    double xx = a.x * a.x;
+    double yy = a.y * a.y;
+    a.r2 = xx + yy;
+    a.accept = !(a.r2 > 1.0 || a.r2 == 0.0);
+    return a;
+}
+
+} // namespace dfamd

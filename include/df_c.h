@@ -1,0 +1,158 @@
+/*
+ * df_c.h — C ABI of the MI355X-native DIGITAL_FILTER (libdfamd.so).
+ *
+ * This is the drop-in boundary for connorswitala/digital-filtering's hot path.
+ * Each entry point replaces one piece of the reference C++ API
+ * (/root/reference/digital-filtering-c++/df/df.hpp); the C++ header df.hpp in
+ * this directory rebuilds that API (DFConfig, FilterField, DIGITAL_FILTER) on
+ * top of these functions, and INTEGRATION.md shows the Fortran / ctypes
+ * bindings a maintainer would add.
+ *
+ * Plain pointers and sizes only. All functions return 0 (DF_OK) on success and
+ * a negative DF_E* code on failure; df_last_error() describes the last failure
+ * of the calling thread. A handle owns one GPU stream and is not thread-safe.
+ */
+#ifndef DF_C_H
+#define DF_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DF_ABI_VERSION 1
+
+enum df_status {
+    DF_OK = 0,
+    DF_EINVAL = -1,   /* bad argument / config                               */
+    DF_EIO = -2,      /* input file missing or malformed (reference: cerr + continue, df.cpp:225-228) */
+    DF_EHIP = -3,     /* HIP runtime / kernel launch failure, or no GPU       */
+    DF_ENOMEM = -4,   /* device allocation failed                             */
+    DF_ERNG = -5,     /* device RNG ran short of polar attempts (never expected) */
+    DF_ECOMM = -6     /* RCCL failure (multi-GPU z-strips)                    */
+};
+
+enum df_plane { DF_PLANE_NATIVE = 0, DF_PLANE_SYNTHETIC = 1 };
+enum df_coeff_mode {
+    DF_COEFF_PACKED = 0, /* stream the per-cell coefficient vectors by/bz from HBM (reference data contract) */
+    DF_COEFF_TABLE = 1   /* read b(N,i) from a per-N table: same values, no B stream */
+};
+enum df_field { DF_U = 0, DF_V = 1, DF_W = 2, DF_T = 3, DF_RHO = 4, DF_FILT_OLD_U = 5, DF_FILT_OLD_V = 6, DF_FILT_OLD_W = 7 };
+enum df_row {
+    DF_ROW_R11 = 0, DF_ROW_R21, DF_ROW_R22, DF_ROW_R33, DF_ROW_US, DF_ROW_TS, DF_ROW_RHOS, DF_ROW_MS, DF_ROW_PS,
+    DF_ROW_YC, DF_ROW_YC_D
+};
+
+/* Mirrors struct DFConfig (df.hpp:38-49) field for field, then extensions.
+ * df_config_default() fills the values the reference constructor hard-codes
+ * (df.cpp:7-16) so an untouched config behaves like the reference. */
+typedef struct df_config_c {
+    double d_i, rho_e, U_e, mu_e;          /* df.hpp:39-42 */
+    int vel_file_offset, vel_file_N_values; /* df.hpp:44-45 (unused by the reference too) */
+    const char *grid_file;                 /* df.hpp:47 (reference has no grid reader; ignored) */
+    const char *vel_fluc_file;             /* df.hpp:48: RST profile (reference reads ../files/RST.dat, df.cpp:224) */
+    /* ---- extensions ---- */
+    const char *line_file;                 /* mean profile (reference ../line.dat, df.cpp:16) */
+    uint64_t seed;                         /* pcg32 seed (reference: random_device, df.cpp:334) */
+    int seed_from_random_device;           /* 1: draw the 32-bit seed from std::random_device like the reference */
+    int plane;                             /* enum df_plane */
+    int Ny, Nz;                            /* synthetic plane size */
+    int N_min, N_max;                      /* synthetic half-width rule */
+    int coeff_mode;                        /* enum df_coeff_mode */
+    const char *csv_path;                  /* non-NULL: write the reference CSV after every df_filter (df.cpp:466-467) */
+    int device;                            /* HIP device ordinal; -1 = host-only handle (setup
+                                              queries only, no GPU: used by CPU tests) */
+    int rank, world;                       /* z-strip partition: this GPU is strip `rank` of `world` */
+    const void *comm_id;                   /* 128-byte RCCL unique id (world > 1), from df_comm_unique_id */
+    int rows_per_wave;                     /* y-pass register blocking (tuning knob, 0 = default) */
+    int rng_resume;                        /* 1: start the stream at (rng_state, rng_saved_flag, rng_saved) */
+    int rng_saved_flag;                    /*    instead of seeding (checkpoint/resume, and continuing */
+    uint64_t rng_state;                    /*    the reference's process-wide stream across instances) */
+    double rng_saved;
+} df_config_c;
+
+typedef struct df_handle df_handle;
+
+typedef struct df_profile {
+    long long calls;      /* df_filter calls timed since df_set_profiling(h, 1) */
+    double rng_ms;        /* summed device time of each phase, milliseconds */
+    double ypass_ms;
+    double halo_ms;
+    double zpass_ms;
+    double total_ms;      /* first event to last event of each call, summed */
+} df_profile;
+
+void df_config_default(df_config_c *cfg);
+
+/* DIGITAL_FILTER::DIGITAL_FILTER(DFConfig) (df.hpp:89, df.cpp:4-66): setup plus
+ * the constructor's step 0 (noise, sweeps, RST scaling; no correlation, no SRA).
+ * Returns NULL on failure. */
+df_handle *df_create(const df_config_c *cfg);
+
+/* DIGITAL_FILTER::filter(double dt) (df.hpp:100, df.cpp:449-468): one timestep.
+ * Asynchronous on the handle's stream unless csv_path is set. */
+int df_filter(df_handle *h, double dt);
+
+/* Several z-strips of one plane held by ONE process (one device each, or several
+ * strips on one device): cfgs[r] has rank r, world n and no comm_id. Creation
+ * runs step 0 for the whole plane; df_filter_group advances all strips by dt
+ * with in-process halo copies instead of RCCL. */
+int df_create_group(const df_config_c *cfgs, int n, df_handle **out);
+int df_filter_group(df_handle **hs, int n, double dt);
+
+/* The reference's public stage functions (df.hpp:96-101), run on the device. */
+int df_generate_white_noise(df_handle *h);          /* df.cpp:332-349 */
+int df_filtering_sweeps(df_handle *h, int comp);    /* df.cpp:351-406, writes filt of one component */
+int df_correlate_fields(df_handle *h, int comp, double dt); /* df.cpp:408-417 */
+int df_apply_RST_scaling(df_handle *h);             /* df.cpp:419-447 */
+int df_get_rho_T_fluc(df_handle *h);                /* df.cpp:470-485 */
+
+/* Host copy of a dense [Ny x Nz_local] field (u.fluc etc., df.hpp:24-34). Synchronizes. */
+int df_get_field(df_handle *h, int which, double *host_out);
+/* Device pointer of the same dense field (row-major, pitch Nz_local doubles). */
+const double *df_device_field(df_handle *h, int which);
+/* Ny, global Nz, and the [z0, z1) columns this handle owns. */
+int df_dims(df_handle *h, int *Ny, int *Nz, int *z0, int *z1);
+/* Per-row profiles (length Ny) and scalars (0 u_tau, 1 tau_w, 2 d_v). */
+int df_get_row(df_handle *h, int which, double *out);
+double df_get_scalar(df_handle *h, int which);
+/* Per-cell half-widths / offsets of one component, reference layout (N_ys, N_zs,
+ * by_offsets, bz_offsets, df.hpp:30-31): out has Ny*Nz_local ints. dir 0 = y, 1 = z. */
+int df_get_halfwidths(df_handle *h, int comp, int dir, int *out);
+int df_get_offsets(df_handle *h, int comp, int dir, int *out);
+/* max half-widths (F.Ny_max, F.Nz_max) and the offset-packed coefficient count. */
+int df_get_comp_info(df_handle *h, int comp, int *Ny_max, int *Nz_max, long long *by_size, long long *bz_size);
+/* Offset-packed coefficients exactly as FilterField::by / bz (df.cpp:151-216). */
+int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n);
+
+/* Process-wide RNG stream of the reference (df.cpp:334-335) is per handle here:
+ * pcg32 state, normal_distribution cached flag and value. Synchronizes. */
+int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved);
+int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved);
+/* Noise arrays as the reference holds them after the sweeps (FilterField r_ys /
+ * r_zs, df.hpp:26): dir 0 -> r_ys, (Ny + 2*Ny_max) x Nz_local; dir 1 -> r_zs,
+ * Ny x (Nz_local + 2*Nz_max) with the z-halo. `n` is the capacity of out. */
+int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n);
+/* Normals drawn per df_filter (the six r_ys/r_zs arrays, df.cpp:343-348). */
+long long df_stream_length(df_handle *h);
+
+/* Timing (hipEvents on the handle's stream). */
+int df_set_profiling(df_handle *h, int on);
+int df_get_profile(df_handle *h, df_profile *out);
+int df_sync(df_handle *h);
+void *df_stream(df_handle *h);
+/* Bytes of HBM the packed/table hot path must move per df_filter (SURVEY 8d model). */
+double df_algorithmic_bytes(df_handle *h, int kernel /* -1 whole call, 0 ypass, 1 zpass */);
+
+int df_comm_unique_id(void *out, size_t len); /* RCCL unique id, len >= 128 */
+
+void df_destroy(df_handle *h);
+const char *df_last_error(void);
+int df_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DF_C_H */

@@ -1,0 +1,126 @@
+"""CPU tests of the product's host logic through the C ABI (host-only handles,
+device = -1): setup rows, half-widths, coefficients, offsets, stream geometry
+and z-strip planning, checked against the reference's golden vectors and the
+oracle. No GPU is touched."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import dfamd
+import oracle as O
+from conftest import GOLDEN
+
+ROWS8 = ("R11", "R21", "R22", "R33", "Us", "Ts", "rhos", "Ms")
+
+
+def host(**kw):
+    return dfamd.DigitalFilter(device=-1, seed=1, **kw)
+
+
+def test_library_exports_every_header_symbol():
+    L = dfamd.lib()
+    syms = dfamd.header_symbols()
+    assert len(syms) >= 30
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+    assert L.df_abi_version() == 1
+
+
+def test_native_setup_matches_reference():
+    g = np.load(os.path.join(GOLDEN, "native_s42.npz"))
+    meta = json.load(open(os.path.join(GOLDEN, "native_s42.json")))
+    f = host()
+    assert (f.Ny, f.Nz) == (meta["Ny"], meta["Nz"])
+    assert f.scalar("u_tau") == meta["u_tau"] and f.scalar("tau_w") == meta["tau_w"]
+    for r in ROWS8:
+        assert np.array_equal(f.row(r), g["row_" + r]), r
+    for c, n in enumerate("uvw"):
+        info = f.comp_info(c)
+        assert info["Ny_max"] == meta["Ny_max"][c] and info["Nz_max"] == meta["Nz_max"][c]
+        assert info["by_size"] == meta["by_size"][c] and info["bz_size"] == meta["bz_size"][c]
+        assert np.array_equal(f.halfwidths(c, "y")[:, 0], g["Ny_" + n])
+        assert np.array_equal(f.halfwidths(c, "z")[:, 0], g["Nz_" + n])
+
+
+@pytest.mark.parametrize("name", ["c1_s42", "ramp256_s1234", "ragged_s7"])
+def test_synthetic_setup_matches_reference(name):
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    f = host(plane="synthetic", Ny=int(g["Ny"]), Nz=int(g["Nz"]), N_min=int(g["N_min"]), N_max=int(g["N_max"]))
+    for r in ROWS8:
+        assert np.array_equal(f.row(r), g["row_" + r]), r
+    for c, n in enumerate("uvw"):
+        assert np.array_equal(f.halfwidths(c, "y")[:, 0], g["Ny_" + n])
+        assert np.array_equal(f.halfwidths(c, "z")[:, 0], g["Nz_" + n])
+
+
+@pytest.mark.parametrize("spec", [dict(), dict(plane="synthetic", Ny=64, Nz=40, N_min=2, N_max=12)])
+def test_coefficients_offsets_and_stream_match_oracle(spec):
+    f = host(**spec)
+    kw = {}
+    if spec:
+        kw = dict(plane=O.PLANE_SYNTHETIC, Ny=spec["Ny"], Nz=spec["Nz"], N_min=spec["N_min"], N_max=spec["N_max"])
+    o = O.Filter(seed=1, **kw)
+    n = o.Ny * o.Nz
+    for c in range(3):
+        F = o.comp(c)
+        by = np.ctypeslib.as_array(F.by, shape=(F.by_size,))
+        bz = np.ctypeslib.as_array(F.bz, shape=(F.bz_size,))
+        assert np.array_equal(f.coeffs(c, "y"), by)
+        assert np.array_equal(f.coeffs(c, "z"), bz)
+        assert np.array_equal(f.offsets(c, "y").ravel(), np.ctypeslib.as_array(F.by_offsets, shape=(n,)))
+        assert np.array_equal(f.offsets(c, "z").ravel(), np.ctypeslib.as_array(F.bz_offsets, shape=(n,)))
+    assert f.stream_length() == sum(O.stream_lengths(o))
+
+
+def test_coefficients_are_unit_energy():
+    # Implicit invariant of df.cpp:166-177: sum_i b_i^2 == 1 for every cell.
+    f = host(plane="synthetic", Ny=32, Nz=4, N_min=2, N_max=64)
+    for c in range(3):
+        b = f.coeffs(c, "y")
+        N = f.halfwidths(c, "y").ravel()
+        pos = 0
+        for n in N:
+            seg = b[pos:pos + 2 * n + 1]
+            assert abs((seg * seg).sum() - 1.0) < 1e-13
+            assert np.array_equal(seg, seg[::-1])
+            pos += 2 * n + 1
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_strip_partition_covers_plane(world):
+    Nz = 1000
+    strips = [dfamd.DigitalFilter(device=-1, seed=1, plane="synthetic", Ny=16, Nz=Nz, N_min=2, N_max=8,
+                                  rank=r, world=world) for r in range(world)]
+    z = [(s.z0, s.z1) for s in strips]
+    assert z[0][0] == 0 and z[-1][1] == Nz
+    assert all(z[i][1] == z[i + 1][0] for i in range(world - 1))
+    assert max(b - a for a, b in z) - min(b - a for a, b in z) <= 1
+    whole = host(plane="synthetic", Ny=16, Nz=Nz, N_min=2, N_max=8)
+    for c in range(3):
+        assert sum(s.comp_info(c)["by_size"] for s in strips) == whole.comp_info(c)["by_size"]
+    # every strip draws the same stream: the RNG is replicated, not split
+    assert {s.stream_length() for s in strips} == {whole.stream_length()}
+
+
+def test_strip_narrower_than_halfwidth_is_rejected():
+    with pytest.raises(dfamd.DFError, match="narrower"):
+        dfamd.DigitalFilter(device=-1, seed=1, plane="synthetic", Ny=16, Nz=20, N_min=2, N_max=16, rank=0, world=4)
+
+
+def test_bad_inputs_fail_fast(tmp_path):
+    with pytest.raises(dfamd.DFError, match="cannot open"):
+        host(rst_file=str(tmp_path / "missing.dat"))
+    bad = tmp_path / "bad.dat"
+    bad.write_text("VARIABLES=x\nZONE f=point\n1 2 3\n")
+    with pytest.raises(dfamd.DFError, match="i="):
+        host(rst_file=str(bad))
+    with pytest.raises(dfamd.DFError, match="synthetic"):
+        host(plane="synthetic", Ny=1, Nz=4, N_min=2, N_max=4)
+
+
+def test_host_only_handle_refuses_gpu_calls():
+    f = host()
+    with pytest.raises(dfamd.DFError, match="host-only"):
+        f.filter(1e-8)

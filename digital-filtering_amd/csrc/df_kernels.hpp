@@ -59,6 +59,7 @@ struct SweepArgs {
     double sa[3], s1a[3];   // sqrt(alpha), sqrt(1-alpha) per component
     int do_corr, do_sra, comps_mask;
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
+    int nt_loads;           // non-temporal loads for the coefficient stream
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.

@@ -121,7 +121,7 @@ def comm_unique_id():
 
 
 def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_mode="packed", device=0,
-                rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=8, rst_file=None, line_file=None,
+                rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=4, rst_file=None, line_file=None,
                 d_i=None, rho_e=None, U_e=None, mu_e=None, resume=None):
     """resume = (pcg state, saved_flag, saved): start the stream there instead of seeding."""
     cfg = _Cfg()

@@ -1,0 +1,87 @@
+// Practical HBM ceiling on this MI355X for the access pattern of the sweeps:
+// streaming 16-B-per-lane reads (global_load_dwordx4, plain and nt), and a
+// 16-B copy for reference. Prints one JSON line. Not part of the product.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const dvec2 *__restrict__ p, size_t n, double *sink)
+{
+    dvec2 acc = {0, 0};
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride * 4) {
+        dvec2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            size_t k = i + u * stride;
+            v[u] = k < n ? (NT ? __builtin_nontemporal_load(p + k) : p[k]) : dvec2{0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    if (acc.x == 123.456 && acc.y == 654.321) *sink = acc.x; // keep loads alive
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const dvec2 *__restrict__ a, dvec2 *__restrict__ b, size_t n)
+{
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) b[i] = a[i];
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+int main(int argc, char **argv)
+{
+    size_t bytes = (argc > 1 ? strtoull(argv[1], 0, 10) : 8ull) << 30;
+    size_t n = bytes / 16;
+    dvec2 *a, *b;
+    double *sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes / 4));
+    CK(hipMalloc(&sink, 8));
+    CK(hipMemset(a, 0x3f, bytes));
+    CK(hipMemset(b, 0, bytes / 4));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    int grids[] = {1024, 2048, 4096, 8192};
+    printf("{\"bytes\": %zu", bytes);
+    for (int nt = 0; nt < 2; ++nt)
+        for (int g : grids) {
+            std::vector<float> t;
+            for (int r = 0; r < 6; ++r) {
+                CK(hipEventRecord(e0));
+                if (nt) hipLaunchKernelGGL(read_kernel<true>, dim3(g), dim3(256), 0, 0, a, n, sink);
+                else hipLaunchKernelGGL(read_kernel<false>, dim3(g), dim3(256), 0, 0, a, n, sink);
+                CK(hipEventRecord(e1));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                if (r) t.push_back(ms);
+            }
+            std::sort(t.begin(), t.end());
+            printf(", \"read%s_g%d_GBps\": %.1f", nt ? "_nt" : "", g, bytes / (t[t.size() / 2] * 1e-3) / 1e9);
+        }
+    {
+        size_t nc = n / 4;
+        std::vector<float> t;
+        for (int r = 0; r < 6; ++r) {
+            CK(hipEventRecord(e0));
+            hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, 0, a, b, nc);
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        printf(", \"copy_GBps\": %.1f", 2.0 * nc * 16 / (t[t.size() / 2] * 1e-3) / 1e9);
+    }
+    printf("}\n");
+    return 0;
+}

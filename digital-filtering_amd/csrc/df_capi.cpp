@@ -94,6 +94,9 @@ struct df_handle {
     // halo
     double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
     size_t halo_elems = 0;
+    // statistics (get_rms)
+    double *rms_acc = nullptr, *rms_tmp = nullptr;
+    long long rms_count = 0;
     // profiling
     bool profiling = false;
     std::vector<PhaseEvents> ev;
@@ -743,6 +746,10 @@ const double *df_device_field(df_handle *h, int which)
     case DF_T: return h->T;
     case DF_RHO: return h->rho;
     case DF_FILT_OLD_U: case DF_FILT_OLD_V: case DF_FILT_OLD_W: return h->c[which - DF_FILT_OLD_U].filt_old;
+    case DF_FILT_U: case DF_FILT_V: case DF_FILT_W:
+        if (h->c[which - DF_FILT_U].filt) return h->c[which - DF_FILT_U].filt;
+        g_err = "filt is only materialized by the stage API (df_filtering_sweeps)";
+        return nullptr;
     }
     g_err = "unknown field";
     return nullptr;
@@ -933,6 +940,52 @@ int df_comm_unique_id(void *out, size_t len)
     ncclUniqueId id;
     NCCL_OR(ncclGetUniqueId(&id));
     std::memcpy(out, &id, sizeof id);
+    return DF_OK;
+}
+
+int df_rms_reset(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    const size_t n = (size_t)h->Ny * h->Nz_loc;
+    int rc;
+    if (!h->rms_acc && (rc = dalloc_t(h, &h->rms_acc, 5 * n))) return rc;
+    if (!h->rms_tmp && (rc = dalloc_t(h, &h->rms_tmp, n))) return rc;
+    HIP_OR(hipMemsetAsync(h->rms_acc, 0, 5 * n * sizeof(double), h->stream), DF_EHIP);
+    h->rms_count = 0;
+    return DF_OK;
+}
+
+int df_rms_add(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    int rc;
+    if (!h->rms_acc && (rc = df_rms_reset(h))) return rc;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(launch_rms_add(sweep_args(h), h->rms_acc, h->stream), DF_EHIP);
+    h->rms_count++;
+    return DF_OK;
+}
+
+int df_rms_get(df_handle *h, int which, double *out)
+{
+    if (!valid_dev(h) || !out || which < DF_U || which > DF_RHO) return fail(DF_EINVAL, "bad argument");
+    if (!h->rms_acc || h->rms_count == 0) return fail(DF_EINVAL, "no df_rms_add since df_rms_reset");
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    const size_t n = (size_t)h->Ny * h->Nz_loc;
+    HIP_OR(launch_rms_finish(h->rms_acc + which * n, h->rms_tmp, n, (double)h->rms_count, h->stream), DF_EHIP);
+    HIP_OR(hipMemcpyAsync(out, h->rms_tmp, n * sizeof(double), hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
+}
+
+long long df_rms_count(df_handle *h) { return valid(h) ? h->rms_count : -1; }
+
+int df_get_vertices(df_handle *h, double *y, double *z)
+{
+    if (!valid(h)) return DF_EINVAL;
+    if (y) std::copy(h->setup.y_vert.begin(), h->setup.y_vert.begin() + h->Ny + 1, y);
+    if (z) std::copy(h->setup.z_vert.begin(), h->setup.z_vert.end(), z);
     return DF_OK;
 }
 

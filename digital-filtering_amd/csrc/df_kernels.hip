@@ -506,6 +506,39 @@ hipError_t launch_stage(const SweepArgs &a, int op, int comp, hipStream_t st)
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------ statistics
+
+__global__ void rms_add_kernel(SweepArgs a, double *__restrict__ acc)
+{
+    const size_t n = (size_t)a.Ny * a.Nz_loc;
+    const double *src[5] = {a.fluc[0], a.fluc[1], a.fluc[2], a.T, a.rho};
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < n; idx += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+            const double x = src[f][idx];
+            acc[f * n + idx] += x * x;
+        }
+    }
+}
+
+__global__ void rms_finish_kernel(const double *__restrict__ acc, double *__restrict__ out, size_t n, double count)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        out[i] = sqrt(acc[i] / count);
+}
+
+hipError_t launch_rms_add(const SweepArgs &a, double *acc, hipStream_t st)
+{
+    hipLaunchKernelGGL(rms_add_kernel, dim3(2048), dim3(256), 0, st, a, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_rms_finish(const double *acc, double *out, size_t n, double count, hipStream_t st)
+{
+    hipLaunchKernelGGL(rms_finish_kernel, dim3(1024), dim3(256), 0, st, acc, out, n, count);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------ K6 z-halo
 
 __global__ void halo_pack_kernel(SweepArgs a, double *__restrict__ sl, double *__restrict__ sr)

@@ -72,6 +72,10 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
 // Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),
 // op 1 apply_RST_scaling (419-447), op 2 get_rho_T_fluc (470-485).
 hipError_t launch_stage(const SweepArgs &a, int op, int comp, hipStream_t st);
+// rms_add (df.cpp:571-582): acc[f][idx] += x_f^2 for u', v', w', T', rho'.
+hipError_t launch_rms_add(const SweepArgs &a, double *acc, hipStream_t st);
+// plot_rms (df.cpp:615-621): out = sqrt(acc / count)
+hipError_t launch_rms_finish(const double *acc, double *out, size_t n, double count, hipStream_t st);
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st);
 hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st);
 

@@ -18,7 +18,8 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "df_c.h")
 
 PLANE = {"native": 0, "synthetic": 1}
 COEFF = {"packed": 0, "table": 1}
-FIELDS = {"u": 0, "v": 1, "w": 2, "T": 3, "rho": 4, "filt_old_u": 5, "filt_old_v": 6, "filt_old_w": 7}
+FIELDS = {"u": 0, "v": 1, "w": 2, "T": 3, "rho": 4, "filt_old_u": 5, "filt_old_v": 6, "filt_old_w": 7,
+          "filt_u": 8, "filt_v": 9, "filt_w": 10}
 ROWS = {"R11": 0, "R21": 1, "R22": 2, "R33": 3, "Us": 4, "Ts": 5, "rhos": 6, "Ms": 7, "Ps": 8, "yc": 9, "yc_d": 10}
 
 
@@ -86,6 +87,11 @@ def lib():
         "df_set_rng_state": (C.c_int, [H, C.c_uint64, C.c_int, C.c_double]),
         "df_stream_length": (C.c_longlong, [H]),
         "df_get_noise": (C.c_int, [H, C.c_int, C.c_int, C.c_void_p, C.c_longlong]),
+        "df_rms_reset": (C.c_int, [H]),
+        "df_rms_add": (C.c_int, [H]),
+        "df_rms_get": (C.c_int, [H, C.c_int, C.c_void_p]),
+        "df_rms_count": (C.c_longlong, [H]),
+        "df_get_vertices": (C.c_int, [H, C.c_void_p, C.c_void_p]),
         "df_set_profiling": (C.c_int, [H, C.c_int]),
         "df_get_profile": (C.c_int, [H, C.POINTER(Profile)]),
         "df_sync": (C.c_int, [H]),
@@ -271,6 +277,24 @@ class DigitalFilter:
 
     def stream_length(self):
         return lib().df_stream_length(self._h)
+
+    # --- statistics (get_rms, df.cpp:566-621)
+    def rms_reset(self):
+        _check(lib().df_rms_reset(self._h))
+
+    def rms_add(self):
+        _check(lib().df_rms_add(self._h))
+
+    def rms(self, name):
+        out = np.empty((self.Ny, self.Nz_loc), dtype=np.float64)
+        _check(lib().df_rms_get(self._h, FIELDS[name], out.ctypes.data))
+        return out
+
+    def vertices(self):
+        y = np.empty(self.Ny + 1)
+        z = np.empty(self.Nz + 1)
+        _check(lib().df_get_vertices(self._h, y.ctypes.data, z.ctypes.data))
+        return y, z
 
     # --- measurement
     def set_profiling(self, on):

@@ -39,7 +39,11 @@ enum df_coeff_mode {
     DF_COEFF_PACKED = 0, /* stream the per-cell coefficient vectors by/bz from HBM (reference data contract) */
     DF_COEFF_TABLE = 1   /* read b(N,i) from a per-N table: same values, no B stream */
 };
-enum df_field { DF_U = 0, DF_V = 1, DF_W = 2, DF_T = 3, DF_RHO = 4, DF_FILT_OLD_U = 5, DF_FILT_OLD_V = 6, DF_FILT_OLD_W = 7 };
+enum df_field {
+    DF_U = 0, DF_V = 1, DF_W = 2, DF_T = 3, DF_RHO = 4,
+    DF_FILT_OLD_U = 5, DF_FILT_OLD_V = 6, DF_FILT_OLD_W = 7,
+    DF_FILT_U = 8, DF_FILT_V = 9, DF_FILT_W = 10 /* stage API only (after df_filtering_sweeps) */
+};
 enum df_row {
     DF_ROW_R11 = 0, DF_ROW_R21, DF_ROW_R22, DF_ROW_R33, DF_ROW_US, DF_ROW_TS, DF_ROW_RHOS, DF_ROW_MS, DF_ROW_PS,
     DF_ROW_YC, DF_ROW_YC_D
@@ -137,6 +141,18 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
 int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n);
 /* Normals drawn per df_filter (the six r_ys/r_zs arrays, df.cpp:343-348). */
 long long df_stream_length(df_handle *h);
+
+/* Statistics path of the reference's get_rms() (df.cpp:566-611): per-cell sums of
+ * u'^2, v'^2, w'^2, T'^2, rho'^2 kept on the device. df_rms_add accumulates the
+ * current fields (rms_add, df.cpp:571-582); df_rms_get returns
+ * sqrt(sum / count) (plot_rms, df.cpp:615-621) for which = DF_U..DF_RHO. */
+int df_rms_reset(df_handle *h);
+int df_rms_add(df_handle *h);
+int df_rms_get(df_handle *h, int which, double *out);
+long long df_rms_count(df_handle *h);
+/* Grid vertices used by the reference's writers: y per vertex row (Ny+1) and
+ * z per vertex column (Nz+1, global); y/z do not vary along the other axis. */
+int df_get_vertices(df_handle *h, double *y, double *z);
 
 /* Timing (hipEvents on the handle's stream). */
 int df_set_profiling(df_handle *h, int on);

@@ -121,6 +121,25 @@ def synth_fixture(name, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, dt2=None, nsteps2=
     json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=1)
 
 
+def rms_fixture(name, seed, synth=None, sample_rows=None, csv_head=12):
+    """The reference driver's own path: DIGITAL_FILTER df(config); df.get_rms() (cpp-main.cpp:12-17)."""
+    with tempfile.TemporaryDirectory() as d:
+        run("rms", RUN_ROOT, seed, d, *(synth or ()))
+        meta = json.load(open(os.path.join(d, "meta.json")))
+        Ny, Nz = meta["Ny"], meta["Nz"]
+        rms = {k: np.fromfile(os.path.join(d, f"rms_{k}.bin")).reshape(Ny, Nz) for k in FIELDS}
+        with open(os.path.join(RUN_ROOT, "files", "cpp_vel_fluc_rms.csv")) as f:
+            head = [next(f) for _ in range(csv_head)]
+    open(os.path.join(OUT, f"{name}_csv_head.txt"), "w").writelines(head)
+    sample_rows = sample_rows or (1, Ny // 4, Ny // 2, Ny - 1)
+    arr = {"seed": seed, "Ny": Ny, "Nz": Nz, "rms_counter": meta["rms_counter"],
+           "synth": np.array(synth or (), dtype=np.int64), "sample_rows": np.array(sample_rows)}
+    for k in FIELDS:
+        arr[f"rms_{k}_stats"] = stats(rms[k])
+        arr[f"rms_{k}_rows"] = rms[k][list(sample_rows)]
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arr)
+
+
 def main():
     if not os.path.exists(HARN):
         sys.exit("reference not built: make -C oracle/ref")
@@ -136,6 +155,8 @@ def main():
     synth_fixture("ramp256_s1234", 1234, 256, 256, 4, 16, 1e-8, 2)
     # ragged plane: odd sizes, Nz smaller than the largest half-width
     synth_fixture("ragged_s7", 7, 37, 5, 2, 10, 1e-8, 2, full_steps=(0, 2), sample_rows=(0, 18, 36))
+    # the reference driver's get_rms() (500 steps at dt = 1e-5) on its native grid
+    rms_fixture("rms_native_s42", 42)
     manifest = {
         "generator": "oracle/gen_golden.py",
         "reference": "connorswitala/digital-filtering @ /root/reference (df.cpp compiled unmodified, "

@@ -219,6 +219,21 @@ int main(int argc, char **argv)
         for (int t = 0; t < nsteps2; ++t, ++s) { df.filter(dt2); dump_state(df, out, "step" + std::to_string(s)); }
         return 0;
     }
+    if (mode == "rms") { // rms <root> <seed> <outdir> [Ny Nz Nmin Nmax]: the reference driver's call (cpp-main.cpp:12-17)
+        std::string out = argv[4];
+        DIGITAL_FILTER df(cfg);
+        if (argc > 8) make_synthetic(df, atoi(argv[5]), atoi(argv[6]), atoi(argv[7]), atoi(argv[8]));
+        df.get_rms(); // 500 x {noise, sweeps, correlate, RST, SRA, rms_add} at dt = 1e-5, then plot_rms
+        size_t n = (size_t)df.n_cells;
+        write_bin(out + "/rms_u.bin", df.u.rms.data(), n * 8);
+        write_bin(out + "/rms_v.bin", df.v.rms.data(), n * 8);
+        write_bin(out + "/rms_w.bin", df.w.rms.data(), n * 8);
+        write_bin(out + "/rms_T.bin", df.T_rms.data(), n * 8);
+        write_bin(out + "/rms_rho.bin", df.rho_rms.data(), n * 8);
+        std::ofstream js(out + "/meta.json");
+        js << "{\"Ny\": " << df.Ny << ", \"Nz\": " << df.Nz << ", \"rms_counter\": " << df.rms_counter << "}\n";
+        return 0;
+    }
     if (mode == "time") { // time <root> <seed> <Ny> <Nz> <Nmin> <Nmax> <dt> <ncalls>
         int Ny = atoi(argv[4]), Nz = atoi(argv[5]), Nmin = atoi(argv[6]), Nmax = atoi(argv[7]);
         double dt = strtod(argv[8], 0);

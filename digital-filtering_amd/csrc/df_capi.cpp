@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <random>
 #include <string>
 #include <vector>
@@ -51,7 +52,8 @@ int fail(int code, const std::string &msg)
 
 struct CompDev {
     int Nyp = 0, Nzp = 0, rz_pitch = 0;
-    double *ry = nullptr, *rz = nullptr, *By = nullptr, *Bz = nullptr;
+    double *ry[2] = {}, *rz[2] = {}; // double-buffered noise: set k%2 feeds call k
+    double *By = nullptr, *Bz = nullptr;
     long long *byoff = nullptr, *bzoff = nullptr;
     int *Ny_row = nullptr, *Nz_row = nullptr;
     double *filt_old = nullptr, *fluc = nullptr, *filt = nullptr;
@@ -61,7 +63,8 @@ struct CompDev {
 };
 
 struct PhaseEvents {
-    hipEvent_t e[5];
+    hipEvent_t e[6]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end
+    bool rng = false;
 };
 
 } // namespace
@@ -73,12 +76,17 @@ struct df_handle {
     int coeff_mode = DF_COEFF_PACKED;
     std::string csv_path;
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;     // sweeps (memory-bound)
+    hipStream_t rng_stream = nullptr; // noise generation for the NEXT call (compute-bound), overlapped
+    hipEvent_t ev_rng[2] = {}, ev_release[2] = {};
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
     int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
     int rows_per_wave = 8;
     int nt_loads = 1; // coefficient stream is read once per call: non-temporal (measured +6%)
+    int heavy_first = 1;
+    int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
+    int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
     CompDev c[3];
     double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr;
     int *tab_off = nullptr;
@@ -86,10 +94,19 @@ struct df_handle {
     RngStateDev *rstate = nullptr; // [2], ping-pong by call parity
     int *counts = nullptr;
     long long *offsets = nullptr;
+    uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
     int *err_dev = nullptr;   // mapped host memory
     int *err_host = nullptr;
-    int rng_blocks = 0;
-    long long calls = 0;      // RNG generations so far (selects the ping-pong slot)
+    int rng_blocks = 0;       // attempt blocks per call (4096 attempts each), same on every rank
+    int rng_chunk = 0;        // blocks counted by each z-strip rank (split counting, SURVEY 8e option A)
+    int own_b0 = 0, own_b1 = 0; // this rank's counted blocks
+    bool split_count = false;
+    ncclComm_t rng_comm = nullptr;           // second communicator: the count all-gather runs on rng_stream
+    hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
+    std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
+    long long gen_launched = 0; // generations enqueued (generation n reads state slot n%2, writes (n+1)%2)
+    long long gen_used = 0;     // generations consumed by a visible step (ctor step 0, filter, stage API)
+    int cur = 0;                // noise set of the current step
     RngGeom geom{};
     // halo
     double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
@@ -133,8 +150,8 @@ SweepArgs sweep_args(df_handle *h)
     SweepArgs a{};
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
-        a.ry[c] = d.ry;
-        a.rz[c] = d.rz;
+        a.ry[c] = d.ry[h->cur];
+        a.rz[c] = d.rz[h->cur];
         a.By[c] = d.By;
         a.Bz[c] = d.Bz;
         a.byoff[c] = d.byoff;
@@ -161,6 +178,7 @@ SweepArgs sweep_args(df_handle *h)
     a.rowc = h->rowc;
     a.comps_mask = 7;
     a.nt_loads = h->nt_loads;
+    a.heavy_first = h->heavy_first;
     return a;
 }
 
@@ -171,27 +189,38 @@ int check_rng_error(df_handle *h)
     return DF_OK;
 }
 
+bool prof_on(df_handle *h) { return h->profiling && h->ev_used < h->ev.size(); }
+
 void ev_record(df_handle *h, int phase)
 {
-    if (!h->profiling) return;
-    if (h->ev_used >= h->ev.size()) return;
-    (void)hipEventRecord(h->ev[h->ev_used].e[phase], h->stream);
+    if (!prof_on(h)) return;
+    (void)hipEventRecord(h->ev[h->ev_used].e[phase], phase >= 4 && h->overlap ? h->rng_stream : h->stream);
+}
+
+int sync_all(df_handle *h)
+{
+    HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
 }
 
 int drain_profile(df_handle *h)
 {
     if (!h->ev_used) return DF_OK;
-    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    int rc = sync_all(h);
+    if (rc) return rc;
     for (size_t i = 0; i < h->ev_used; ++i) {
-        float t[4] = {0, 0, 0, 0}, tot = 0;
-        for (int p = 0; p < 4; ++p) (void)hipEventElapsedTime(&t[p], h->ev[i].e[p], h->ev[i].e[p + 1]);
-        (void)hipEventElapsedTime(&tot, h->ev[i].e[0], h->ev[i].e[4]);
-        h->prof.rng_ms += t[0];
-        h->prof.ypass_ms += t[1];
-        h->prof.halo_ms += t[2];
-        h->prof.zpass_ms += t[3];
+        float t[3] = {0, 0, 0}, tot = 0, r = 0;
+        for (int p = 0; p < 3; ++p) (void)hipEventElapsedTime(&t[p], h->ev[i].e[p], h->ev[i].e[p + 1]);
+        (void)hipEventElapsedTime(&tot, h->ev[i].e[0], h->ev[i].e[3]);
+        if (h->ev[i].rng) (void)hipEventElapsedTime(&r, h->ev[i].e[4], h->ev[i].e[5]);
+        h->prof.rng_ms += r;
+        h->prof.ypass_ms += t[0];
+        h->prof.halo_ms += t[1];
+        h->prof.zpass_ms += t[2];
         h->prof.total_ms += tot;
         h->prof.calls++;
+        h->ev[i].rng = false;
     }
     h->ev_used = 0;
     return DF_OK;
@@ -199,13 +228,117 @@ int drain_profile(df_handle *h)
 
 // ---------------------------------------------------------------- phases
 
-int phase_rng(df_handle *h)
+// Noise pipeline. The reference draws all six noise arrays at the start of each
+// call (df.cpp:453); the draws depend only on the stream state, so generation n+1
+// is enqueued on rng_stream as soon as call n's sweeps are enqueued, into the
+// other noise set, and runs (compute-bound) under call n's memory-bound sweeps.
+int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
 {
-    const int in = (int)(h->calls & 1), out = in ^ 1;
-    HIP_OR(launch_rng(h->geom, h->rstate + in, h->rstate + out, h->counts, h->offsets, h->err_dev, h->rng_blocks,
-                      h->stream),
+    const int set = (int)(h->gen_launched & 1);
+    rs = h->overlap ? h->rng_stream : h->stream;
+    HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
+    g = h->geom;
+    for (int c = 0; c < 3; ++c) {
+        g.ry[c] = h->c[c].ry[set];
+        g.rz[c] = h->c[c].rz[set];
+    }
+    if (prof_on(h)) {
+        ev_record(h, 4);
+        h->ev[h->ev_used].rng = true;
+    }
+    const RngStateDev *in = h->rstate + (h->gen_launched & 1);
+    if (!h->split_count)
+        HIP_OR(launch_rng_count(g, in, h->counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs), DF_EHIP);
+    else
+        HIP_OR(launch_rng_count(g, in, h->counts, h->masks, h->rank * h->rng_chunk, h->rng_chunk, h->rng_blocks, rs),
+               DF_EHIP);
+    return DF_OK;
+}
+
+int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
+{
+    const int set = (int)(h->gen_launched & 1);
+    const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
+    HIP_OR(launch_rng_finish(g, h->rstate + (h->gen_launched & 1), h->rstate + ((h->gen_launched + 1) & 1),
+                             h->counts, h->offsets, h->masks, h->err_dev, h->rng_blocks, nb_scan,
+                             h->split_count ? h->own_b0 : 0, h->split_count ? h->own_b1 : h->rng_blocks, rs),
            DF_EHIP);
-    h->calls++;
+    if (prof_on(h)) ev_record(h, 5);
+    HIP_OR(hipEventRecord(h->ev_rng[set], rs), DF_EHIP);
+    h->gen_launched++;
+    return DF_OK;
+}
+
+// In-process strip group: every member counts its share, the shares are copied
+// device to device (the all-gather), then every member scans and generates.
+int launch_gen_group(std::vector<df_handle *> &hs)
+{
+    const int n = (int)hs.size();
+    std::vector<RngGeom> gs(n);
+    std::vector<hipStream_t> rss(n);
+    int rc;
+    for (int r = 0; r < n; ++r) {
+        HIP_OR(hipSetDevice(hs[r]->device), DF_EHIP);
+        if ((rc = gen_begin(hs[r], gs[r], rss[r]))) return rc;
+        HIP_OR(hipEventRecord(hs[r]->ev_counted, rss[r]), DF_EHIP);
+    }
+    for (int r = 0; r < n; ++r) {
+        df_handle *h = hs[r];
+        HIP_OR(hipSetDevice(h->device), DF_EHIP);
+        for (int o = 0; o < n; ++o) {
+            if (o == r) continue;
+            const size_t at = (size_t)o * h->rng_chunk;
+            HIP_OR(hipStreamWaitEvent(rss[r], hs[o]->ev_counted, 0), DF_EHIP);
+            HIP_OR(hipMemcpyAsync(h->counts + at, hs[o]->counts + at, h->rng_chunk * sizeof(int), hipMemcpyDefault,
+                                  rss[r]),
+                   DF_EHIP);
+        }
+        if ((rc = gen_end(h, gs[r], rss[r]))) return rc;
+    }
+    return DF_OK;
+}
+
+// Noise pipeline. The reference draws all six noise arrays at the start of each
+// call (df.cpp:453); the draws depend only on the stream state, so generation n+1
+// is enqueued on rng_stream as soon as call n's sweeps are enqueued, into the
+// other noise set, and runs (compute-bound) under call n's memory-bound sweeps.
+int launch_gen(df_handle *h)
+{
+    if (h->group) return launch_gen_group(*h->group);
+    RngGeom g;
+    hipStream_t rs;
+    int rc = gen_begin(h, g, rs);
+    if (rc) return rc;
+    if (h->split_count) {
+        int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
+        if (h->rng_comm) { // the one collective of the RNG: per-block accept counts
+            NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
+        } else { // DFAMD_SOLO_STRIP timing mode: stand-in counts for the other ranks' shares
+            for (int o = 0; o < h->world; ++o)
+                if (o != h->rank)
+                    HIP_OR(hipMemcpyAsync(h->counts + (size_t)o * h->rng_chunk, mine, h->rng_chunk * sizeof(int),
+                                          hipMemcpyDeviceToDevice, rs),
+                           DF_EHIP);
+        }
+    }
+    return gen_end(h, g, rs);
+}
+
+// Start a visible step on the next generation (reference: generate_white_noise()).
+int consume_gen(df_handle *h)
+{
+    if (h->gen_used > 0) HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP); // previous set free
+    int rc;
+    if (h->gen_launched == h->gen_used && (rc = launch_gen(h))) return rc;
+    h->cur = (int)(h->gen_used & 1);
+    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[h->cur], 0), DF_EHIP);
+    h->gen_used++;
+    return DF_OK;
+}
+
+int prefetch_gen(df_handle *h)
+{
+    if (h->overlap && h->gen_launched == h->gen_used) return launch_gen(h);
     return DF_OK;
 }
 
@@ -239,7 +372,7 @@ int phase_halo_unpack(df_handle *h)
 
 int phase_halo_rccl(df_handle *h)
 {
-    if (h->world == 1) return DF_OK;
+    if (h->world == 1 || h->solo_strip) return DF_OK;
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
     int rc = phase_halo_pack(h);
     if (rc) return rc;
@@ -318,7 +451,13 @@ int build(df_handle *h, const df_config_c *cfg)
     h->world = cfg->world < 1 ? 1 : cfg->world;
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
     h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : 4;
-    if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e); // tuning experiments
+    // tuning knobs for in-process A/B experiments (tools/ab.py); defaults are the measured best
+    if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_HEAVY_FIRST")) h->heavy_first = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
+    if (h->solo_strip) h->split_count = true;
+    if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
     if (h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 && h->rows_per_wave != 8)
         return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
 
@@ -363,9 +502,20 @@ int build(df_handle *h, const df_config_c *cfg)
         g.seg[2 * c + 2] = g.seg[2 * c + 1] + Lz;
     }
     g.Q = g.seg[6];
+    for (int sidx = 0; sidx < 6; ++sidx) {
+        const int c = sidx >> 1;
+        const uint32_t W = (sidx & 1) ? (uint32_t)(s.Nz + 2 * h->c[c].Nzp) : (uint32_t)s.Nz;
+        g.width[sidx] = W;
+        g.rows[sidx] = (sidx & 1) ? (uint32_t)Ny : (uint32_t)(Ny + 2 * h->c[c].Nyp);
+        // ceil(2^64 / W): floor(p * inv / 2^64) == p / W for every p < 2^32
+        g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
+    }
     const PcgJump hop = pcg_jump(4ull * (kRngThreads - 1));
     g.hop_mult = hop.mult;
     g.hop_plus = hop.plus;
+    const PcgJump next = pcg_jump(4ull * kRngThreads); // attempt start -> the thread's next attempt start
+    g.next_mult = next.mult;
+    g.next_plus = next.plus;
     g.Nz_g = s.Nz;
     g.Pz = h->Pz;
     g.z0 = h->z0;
@@ -389,7 +539,18 @@ int build(df_handle *h, const df_config_c *cfg)
     if (cfg->device >= ndev) return fail(DF_EINVAL, "device ordinal out of range");
     h->device = cfg->device;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
-    HIP_OR(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking), DF_EHIP);
+    // Sweeps on the high-priority queue, noise for the next call on the low one:
+    // the memory-bound sweeps keep their waves; the compute-bound RNG fills gaps.
+    int prio_lo = 0, prio_hi = 0;
+    HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
+    int use_prio = 0; // measured: priorities cost 1-2% wall time (profiles/r1/ab_prio_*.json)
+    if (const char *e = std::getenv("DFAMD_RNG_PRIO")) use_prio = std::atoi(e);
+    HIP_OR(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, use_prio ? prio_hi : 0), DF_EHIP);
+    HIP_OR(hipStreamCreateWithPriority(&h->rng_stream, hipStreamNonBlocking, use_prio ? prio_lo : 0), DF_EHIP);
+    for (int set = 0; set < 2; ++set) {
+        HIP_OR(hipEventCreateWithFlags(&h->ev_rng[set], hipEventDisableTiming), DF_EHIP);
+        HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], hipEventDisableTiming), DF_EHIP);
+    }
 
     // ---- per-N coefficient table
     std::vector<int> tab_off_h;
@@ -429,8 +590,10 @@ int build(df_handle *h, const df_config_c *cfg)
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
         const ComponentSetup &F = s.comp[c];
-        if ((rc = dalloc_t(h, &d.ry, (size_t)(Ny + 2 * d.Nyp) * h->Pz))) return rc;
-        if ((rc = dalloc_t(h, &d.rz, (size_t)Ny * d.rz_pitch))) return rc;
+        for (int set = 0; set < 2; ++set) {
+            if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp) * h->Pz))) return rc;
+            if ((rc = dalloc_t(h, &d.rz[set], (size_t)Ny * d.rz_pitch))) return rc;
+        }
         if ((rc = dalloc_t(h, &d.filt_old, n_loc))) return rc;
         if ((rc = dalloc_t(h, &d.fluc, n_loc))) return rc;
         if ((rc = dalloc_t(h, &d.Ny_row, Ny))) return rc;
@@ -464,14 +627,37 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = dalloc_t(h, &h->rho, n_loc))) return rc;
 
     for (int c = 0; c < 3; ++c) {
-        g.ry[c] = h->c[c].ry;
-        g.rz[c] = h->c[c].rz;
         g.Nzp[c] = h->c[c].Nzp;
         g.rz_pitch[c] = h->c[c].rz_pitch;
     }
     if ((rc = dalloc_t(h, &h->rstate, 2))) return rc;
-    if ((rc = dalloc_t(h, &h->counts, h->rng_blocks))) return rc;
-    if ((rc = dalloc_t(h, &h->offsets, h->rng_blocks))) return rc;
+    h->rng_chunk = (h->rng_blocks + h->world - 1) / h->world;
+    const int nb_pad = h->rng_chunk * h->world;
+    h->own_b0 = std::min(h->rank * h->rng_chunk, h->rng_blocks);
+    h->own_b1 = std::min(h->own_b0 + h->rng_chunk, h->rng_blocks);
+    if ((rc = dalloc_t(h, &h->counts, nb_pad))) return rc;
+    if ((rc = dalloc_t(h, &h->offsets, nb_pad))) return rc;
+    if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
+    HIP_OR(hipEventCreateWithFlags(&h->ev_counted, hipEventDisableTiming), DF_EHIP);
+    {
+        // jump tables: block b starts 4*4096*b outputs in, thread tid 4*tid further
+        auto compose = [](PcgJumpDev a, PcgJump b) { // b after a
+            return PcgJumpDev{b.mult * a.mult, b.mult * a.plus + b.plus};
+        };
+        std::vector<PcgJumpDev> jb(nb_pad), jt(kRngThreads);
+        const PcgJump blk = pcg_jump(4ull * kRngBlockAttempts), one = pcg_jump(4);
+        jb[0] = PcgJumpDev{1, 0};
+        for (int b = 1; b < nb_pad; ++b) jb[b] = compose(jb[b - 1], blk);
+        jt[0] = PcgJumpDev{1, 0};
+        for (int t = 1; t < kRngThreads; ++t) jt[t] = compose(jt[t - 1], one);
+        PcgJumpDev *djb = nullptr, *djt = nullptr;
+        if ((rc = dalloc_t(h, &djb, jb.size()))) return rc;
+        if ((rc = dalloc_t(h, &djt, jt.size()))) return rc;
+        if ((rc = upload(h, djb, jb.data(), jb.size()))) return rc;
+        if ((rc = upload(h, djt, jt.data(), jt.size()))) return rc;
+        h->geom.jump_block = djb;
+        h->geom.jump_thread = djt;
+    }
     HIP_OR(hipHostMalloc((void **)&h->err_host, sizeof(int), hipHostMallocMapped), DF_EHIP);
     *h->err_host = 0;
     HIP_OR(hipHostGetDevicePointer((void **)&h->err_dev, h->err_host, 0), DF_EHIP);
@@ -494,8 +680,11 @@ int build(df_handle *h, const df_config_c *cfg)
             ncclUniqueId id;
             std::memcpy(&id, cfg->comm_id, sizeof(id));
             NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
+            NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
+            h->split_count = true;
         }
     }
+    for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     return DF_OK;
 }
@@ -504,11 +693,12 @@ int step0(df_handle *h)
 {
     // Constructor step 0 (df.cpp:57-62): noise, sweeps, RST; no correlation, no SRA.
     int rc;
-    if ((rc = phase_rng(h))) return rc;
+    if ((rc = consume_gen(h))) return rc;
     if ((rc = phase_ypass(h, 7))) return rc;
     if ((rc = phase_halo_rccl(h))) return rc;
     if ((rc = phase_zpass(h, false, false, 0.0))) return rc;
-    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    if ((rc = prefetch_gen(h))) return rc;
+    if ((rc = sync_all(h))) return rc;
     return check_rng_error(h);
 }
 
@@ -516,11 +706,19 @@ void destroy(df_handle *h)
 {
     if (!h) return;
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
     for (void *p : h->allocs) (void)hipFree(p);
     if (h->err_host) (void)hipHostFree(h->err_host);
+    if (h->rng_comm) ncclCommDestroy(h->rng_comm);
     if (h->comm) ncclCommDestroy(h->comm);
+    if (h->ev_counted) (void)hipEventDestroy(h->ev_counted);
+    for (int set = 0; set < 2; ++set) {
+        if (h->ev_rng[set]) (void)hipEventDestroy(h->ev_rng[set]);
+        if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
+    }
+    if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -540,7 +738,7 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         df_handle *h = hs[r];
         HIP_OR(hipSetDevice(h->device), DF_EHIP);
         if ((rc = check_rng_error(h))) return rc;
-        if ((rc = phase_rng(h))) return rc;
+        if ((rc = consume_gen(h))) return rc;
         if ((rc = phase_ypass(h, 7))) return rc;
         if ((rc = phase_halo_pack(h))) return rc;
     }
@@ -553,9 +751,10 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         if (r < n - 1) HIP_OR(hipMemcpyAsync(h->recv_r, hs[r + 1]->send_l, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
         if ((rc = phase_halo_unpack(h))) return rc;
         if ((rc = phase_zpass(h, corr_sra, corr_sra, dt))) return rc;
+        if ((rc = prefetch_gen(h))) return rc;
     }
     for (int r = 0; r < n; ++r) {
-        HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
+        if ((rc = sync_all(hs[r]))) return rc;
         if ((rc = check_rng_error(hs[r]))) return rc;
         if (corr_sra && (rc = write_csv_if(hs[r]))) return rc;
     }
@@ -617,7 +816,7 @@ df_handle *df_create(const df_config_c *cfg)
     df_handle *h = new df_handle();
     int rc = DF_OK;
     if (cfg->device < 0 && cfg->world > 1 && !cfg->comm_id) rc = DF_OK; // host-only strip planning
-    else if (cfg->world > 1 && !cfg->comm_id)
+    else if (cfg->world > 1 && !cfg->comm_id && !(std::getenv("DFAMD_SOLO_STRIP") && std::atoi(std::getenv("DFAMD_SOLO_STRIP"))))
         rc = fail(DF_EINVAL, "world > 1 needs comm_id (RCCL) or df_create_group (in-process strips)");
     if (rc == DF_OK) rc = build(h, cfg);
     if (rc == DF_OK && h->device >= 0) rc = step0(h);
@@ -636,18 +835,19 @@ int df_filter(df_handle *h, double dt)
     if (!valid_dev(h)) return DF_EINVAL;
     int rc = check_rng_error(h);
     if (rc) return rc;
-    if (h->world > 1 && !h->comm) return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
+    if (h->world > 1 && !h->comm && !h->solo_strip)
+        return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
-    const bool prof = h->profiling && h->ev_used < h->ev.size();
+    const bool prof = prof_on(h);
+    if ((rc = consume_gen(h))) return rc;
     ev_record(h, 0);
-    if ((rc = phase_rng(h))) return rc;
-    ev_record(h, 1);
     if ((rc = phase_ypass(h, 7))) return rc;
-    ev_record(h, 2);
+    ev_record(h, 1);
     if ((rc = phase_halo_rccl(h))) return rc;
-    ev_record(h, 3);
+    ev_record(h, 2);
     if ((rc = phase_zpass(h, true, true, dt))) return rc;
-    ev_record(h, 4);
+    ev_record(h, 3);
+    if ((rc = prefetch_gen(h))) return rc; // next call's noise, under this call's sweeps
     if (prof) h->ev_used++;
     return write_csv_if(h);
 }
@@ -667,6 +867,13 @@ int df_create_group(const df_config_c *cfgs, int n, df_handle **out)
         out[r] = new df_handle();
         rc = build(out[r], &cfgs[r]);
     }
+    if (rc == DF_OK && n > 1) {
+        auto grp = std::make_shared<std::vector<df_handle *>>(out, out + n);
+        for (int r = 0; r < n; ++r) {
+            out[r]->group = grp;
+            out[r]->split_count = true; // each strip counts 1/n of the attempts (SURVEY 8e option A)
+        }
+    }
     if (rc == DF_OK) rc = group_step(out, n, false, 0.0); // the constructor's step 0
     if (rc != DF_OK) {
         std::string keep = g_err;
@@ -682,7 +889,8 @@ int df_create_group(const df_config_c *cfgs, int n, df_handle **out)
 int df_generate_white_noise(df_handle *h)
 {
     if (!valid_dev(h)) return DF_EINVAL;
-    return phase_rng(h);
+    int rc = consume_gen(h);
+    return rc ? rc : prefetch_gen(h);
 }
 
 int df_filtering_sweeps(df_handle *h, int comp)
@@ -851,8 +1059,12 @@ int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
 {
     if (!valid_dev(h)) return DF_EINVAL;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
-    RngStateDev st;
-    HIP_OR(hipMemcpyAsync(&st, h->rstate + (h->calls & 1), sizeof st, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    int rc = sync_all(h);
+    if (rc) return rc;
+    RngStateDev st; // state after the last visible step: slot gen_used % 2 (a prefetched
+                    // generation writes the other slot)
+    HIP_OR(hipMemcpyAsync(&st, h->rstate + (h->gen_used & 1), sizeof st, hipMemcpyDeviceToHost, h->stream),
+           DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     if (state) *state = st.state;
     if (saved_flag) *saved_flag = st.saved_flag;
@@ -863,10 +1075,17 @@ int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
 int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
 {
     if (!valid_dev(h)) return DF_EINVAL;
+    if (h->group) return fail(DF_EINVAL, "df_set_rng_state on a member of an in-process strip group");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    int rc = sync_all(h);
+    if (rc) return rc;
     RngStateDev st{state, saved_flag ? 1 : 0, 0, saved};
-    HIP_OR(hipMemcpyAsync(h->rstate + (h->calls & 1), &st, sizeof st, hipMemcpyHostToDevice, h->stream), DF_EHIP);
+    HIP_OR(hipMemcpyAsync(h->rstate + (h->gen_used & 1), &st, sizeof st, hipMemcpyHostToDevice, h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    if (h->gen_launched > h->gen_used) { // the prefetched noise came from the old state: redo it
+        h->gen_launched = h->gen_used;
+        if ((rc = launch_gen(h))) return rc;
+    }
     return DF_OK;
 }
 
@@ -897,8 +1116,8 @@ int df_get_profile(df_handle *h, df_profile *out)
 int df_sync(df_handle *h)
 {
     if (!valid_dev(h)) return DF_EINVAL;
-    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
-    return check_rng_error(h);
+    int rc = sync_all(h);
+    return rc ? rc : check_rng_error(h);
 }
 
 void *df_stream(df_handle *h) { return valid_dev(h) ? (void *)h->stream : nullptr; }
@@ -911,7 +1130,7 @@ int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n)
     const int rows = dir ? h->Ny : h->Ny + 2 * d.Nyp;
     if (n < (long long)width * rows) return fail(DF_EINVAL, "output too small");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
-    HIP_OR(hipMemcpy2DAsync(out, (size_t)width * 8, dir ? d.rz : d.ry, (size_t)(dir ? d.rz_pitch : h->Pz) * 8,
+    HIP_OR(hipMemcpy2DAsync(out, (size_t)width * 8, dir ? d.rz[h->cur] : d.ry[h->cur], (size_t)(dir ? d.rz_pitch : h->Pz) * 8,
                             (size_t)width * 8, rows, hipMemcpyDeviceToHost, h->stream),
            DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);

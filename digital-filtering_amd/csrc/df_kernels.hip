@@ -68,31 +68,45 @@ hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_ro
 // so consecutive lanes hold consecutive attempts and a wave's accepted attempts
 // map to consecutive stream positions (coalesced stores).
 
-__device__ __forceinline__ uint64_t thread_first_state(uint64_t S, int b, int tid)
+// State at the thread's first attempt, advance(S, 4*(b*4096 + tid)), as two
+// affine steps from host-built jump tables (pcg_random.hpp:639-662 composed).
+__device__ __forceinline__ uint64_t thread_first_state(const RngGeom &g, uint64_t S, int b, int tid)
 {
-    return pcg_advance(S, 4ull * ((uint64_t)b * kRngBlockAttempts + (uint64_t)tid));
+    const PcgJumpDev jb = g.jump_block[b], jt = g.jump_thread[tid];
+    return jt.mult * (jb.mult * S + jb.plus) + jt.plus;
 }
 
+// Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
+// the last z-strip rank's share) report zero.
 __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                               int *__restrict__ counts)
+                                                               int *__restrict__ counts,
+                                                               uint16_t *__restrict__ masks, int b0, int nb_total)
 {
     __shared__ int wsum[kRngThreads / 64];
     const int tid = threadIdx.x;
-    uint64_t st = thread_first_state(sin->state, blockIdx.x, tid);
+    const int gb = b0 + blockIdx.x;
+    if (gb >= nb_total) {
+        if (tid == 0) counts[gb] = 0;
+        return;
+    }
+    uint64_t st = thread_first_state(g, sin->state, gb, tid);
     int cnt = 0;
+    uint32_t bits = 0;
 #pragma unroll 4
     for (int m = 0; m < kRngPerThread; ++m) {
         PolarAttempt a = polar_attempt(st);
         cnt += a.accept ? 1 : 0;
+        bits |= (a.accept ? 1u : 0u) << m;
         st = g.hop_mult * st + g.hop_plus;
     }
+    masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
     if ((tid & 63) == 0) wsum[tid >> 6] = cnt;
     __syncthreads();
     if (tid == 0) {
         int t = 0;
         for (int w = 0; w < kRngThreads / 64; ++w) t += wsum[w];
-        counts[blockIdx.x] = t;
+        counts[gb] = t;
     }
 }
 
@@ -127,61 +141,170 @@ __global__ __launch_bounds__(1024) void rng_scan_kernel(const int *__restrict__ 
     }
 }
 
-// Stream position q -> destination in this GPU's buffers, or nullptr if the
-// reference draws that normal but this GPU never reads it (the r_zs interior,
-// df.cpp:377 overwrites it; columns owned by other GPUs).
-__device__ __forceinline__ double *stream_dest(const RngGeom &g, uint64_t q)
+// The stream-layout tables of RngGeom, staged in LDS by the generate kernel:
+// indexing kernel arguments with a per-lane array index compiles to global
+// loads (and vmcnt stalls) inside the hot loop; LDS reads do not.
+struct StreamTables {
+    uint64_t seg[7];
+    uint64_t inv_width[6];
+    uint32_t width[6], rows[6];
+    double *ry[3], *rz[3];
+    int Nzp[3], rz_pitch[3];
+    int Nz_g, Pz, z0, z1, is_first, is_last;
+};
+
+// A stream position q as (array, row, column) of the reference's six arrays.
+struct StreamPos {
+    int sidx;
+    uint32_t row, col;
+};
+
+template <class G> __device__ __forceinline__ StreamPos stream_pos(const G &g, uint64_t q)
 {
     int sidx = 0;
 #pragma unroll
     for (int s = 1; s < 6; ++s) sidx += (q >= g.seg[s]) ? 1 : 0;
     const uint32_t p = (uint32_t)(q - g.seg[sidx]);
-    const int c = sidx >> 1;
-    if ((sidx & 1) == 0) { // r_ys: Nz_g columns per row
-        const uint32_t row = p / (uint32_t)g.Nz_g;
-        const int col = (int)(p - row * (uint32_t)g.Nz_g);
-        if (col < g.z0 || col >= g.z1) return nullptr;
-        return g.ry[c] + (size_t)row * g.Pz + (col - g.z0);
+    const uint32_t W = g.width[sidx];
+    const uint32_t row = (W == 1) ? p : (uint32_t)__umul64hi((uint64_t)p, g.inv_width[sidx]);
+    return {sidx, row, p - row * W};
+}
+
+template <class G> __device__ __forceinline__ StreamPos stream_next(const G &g, StreamPos s)
+{
+    if (++s.col == g.width[s.sidx]) {
+        s.col = 0;
+        if (++s.row == g.rows[s.sidx]) {
+            s.row = 0;
+            ++s.sidx;
+        }
     }
-    const uint32_t W = (uint32_t)(g.Nz_g + 2 * g.Nzp[c]);
-    const uint32_t row = p / W;
-    const int gc = (int)(p - row * W);
+    return s;
+}
+
+// Destination in this GPU's buffers, or nullptr if the reference draws that
+// normal but this GPU never reads it (the r_zs interior, which df.cpp:377
+// overwrites; columns owned by other GPUs).
+template <class G> __device__ __forceinline__ double *stream_dest(const G &g, StreamPos s)
+{
+    const int c = s.sidx >> 1;
+    const int col = (int)s.col;
+    if ((s.sidx & 1) == 0) { // r_ys: Nz_g columns per row
+        if (col < g.z0 || col >= g.z1) return nullptr;
+        return g.ry[c] + (size_t)s.row * g.Pz + (col - g.z0);
+    }
     int lc;
-    if (gc < g.Nzp[c]) {
+    if (col < g.Nzp[c]) {
         if (!g.is_first) return nullptr;
-        lc = gc;
-    } else if (gc >= g.Nzp[c] + g.Nz_g) {
+        lc = col;
+    } else if (col >= g.Nzp[c] + g.Nz_g) {
         if (!g.is_last) return nullptr;
-        lc = gc - g.z0;
+        lc = col - g.z0;
     } else {
         return nullptr;
     }
-    return g.rz[c] + (size_t)row * g.rz_pitch[c] + lc;
+    return g.rz[c] + (size_t)s.row * g.rz_pitch[c] + lc;
+}
+
+// Does [a, b) (offsets inside one row-major array of rows of width W) hit a
+// column in [c0, c1)?
+__device__ __forceinline__ bool span_hits_cols(uint32_t a, uint32_t b, uint32_t W, uint32_t c0, uint32_t c1)
+{
+    if (c0 >= c1 || a >= b) return false;
+    const uint32_t ra = a / W, rb = (b - 1) / W;
+    const uint32_t ca = a - ra * W, cb = (b - 1) - rb * W;
+    if (rb > ra + 1) return true; // a full row in between
+    if (rb == ra) return ca < c1 && cb >= c0;
+    return ca < c1 || cb >= c0; // [ca, W) then [0, cb]
+}
+
+// Does the stream range [q0, q1) hold a normal this GPU stores? (z-strips:
+// blocks of attempts that only feed other GPUs' columns skip their pass 2.)
+template <class G> __device__ bool range_needed(const G &g, uint64_t q0, uint64_t q1)
+{
+    for (int sidx = 0; sidx < 6; ++sidx) {
+        const uint64_t lo = q0 > g.seg[sidx] ? q0 : g.seg[sidx];
+        const uint64_t hi = q1 < g.seg[sidx + 1] ? q1 : g.seg[sidx + 1];
+        if (lo >= hi) continue;
+        const uint32_t a = (uint32_t)(lo - g.seg[sidx]), b = (uint32_t)(hi - g.seg[sidx]);
+        const uint32_t W = g.width[sidx];
+        if ((sidx & 1) == 0) {
+            if (span_hits_cols(a, b, W, (uint32_t)g.z0, (uint32_t)g.z1)) return true;
+        } else {
+            const uint32_t nzp = (uint32_t)g.Nzp[sidx >> 1];
+            if (g.is_first && span_hits_cols(a, b, W, 0, nzp)) return true;
+            if (g.is_last && span_hits_cols(a, b, W, nzp + (uint32_t)g.Nz_g, W)) return true;
+        }
+    }
+    return false;
 }
 
 __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                   RngStateDev *__restrict__ sout,
-                                                                  const long long *__restrict__ offsets)
+                                                                  const long long *__restrict__ offsets,
+                                                                  const uint16_t *__restrict__ masks,
+                                                                  const int *__restrict__ counts, int own_b0,
+                                                                  int own_b1)
 {
     __shared__ int cnt[kRngPerThread][kRngThreads / 64];
     __shared__ int pre[kRngPerThread][kRngThreads / 64];
+    __shared__ StreamTables T;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
     const long long Ob = offsets[blockIdx.x];
-    if (Ob >= A) return;
+    if (Ob >= A) return; // uniform: the whole block is past the call's last attempt
+    {
+        // Blocks whose normals all land on other GPUs' columns (or in the r_zs
+        // interior) have nothing to store; the one holding the last accepted
+        // attempt still records the stream state.
+        const long long Oe = Ob + counts[blockIdx.x];
+        const uint64_t q_lo = f + 2ull * (uint64_t)Ob;
+        const uint64_t q_hi = (f + 2ull * (uint64_t)Oe) < g.Q ? (f + 2ull * (uint64_t)Oe) : g.Q;
+        const bool holds_last = Oe >= A;
+        if (!holds_last && !(blockIdx.x == 0 && f) && !range_needed(g, q_lo, q_hi)) return;
+    }
+    if (tid == 0) {
+        for (int i = 0; i < 7; ++i) T.seg[i] = g.seg[i];
+        for (int i = 0; i < 6; ++i) {
+            T.inv_width[i] = g.inv_width[i];
+            T.width[i] = g.width[i];
+            T.rows[i] = g.rows[i];
+        }
+        for (int c = 0; c < 3; ++c) {
+            T.ry[c] = g.ry[c];
+            T.rz[c] = g.rz[c];
+            T.Nzp[c] = g.Nzp[c];
+            T.rz_pitch[c] = g.rz_pitch[c];
+        }
+        T.Nz_g = g.Nz_g;
+        T.Pz = g.Pz;
+        T.z0 = g.z0;
+        T.z1 = g.z1;
+        T.is_first = g.is_first;
+        T.is_last = g.is_last;
+    }
+    __syncthreads();
 
     if (blockIdx.x == 0 && tid == 0 && f) {
-        double *d = stream_dest(g, 0);
+        double *d = stream_dest(T, stream_pos(T, 0));
         if (d) *d = sin->saved * 1.0 + 0.0;
     }
-    const uint64_t st0 = thread_first_state(sin->state, blockIdx.x, tid);
-    uint64_t st = st0;
+    uint32_t bits;
+    if ((int)blockIdx.x >= own_b0 && (int)blockIdx.x < own_b1) {
+        bits = masks[(size_t)blockIdx.x * kRngThreads + tid]; // this rank counted the block (K1)
+    } else { // another z-strip rank counted it: redo its accept tests
+        bits = 0;
+        uint64_t sc = thread_first_state(g, sin->state, blockIdx.x, tid);
+        for (int m = 0; m < kRngPerThread; ++m) {
+            bits |= (polar_attempt(sc).accept ? 1u : 0u) << m;
+            sc = g.hop_mult * sc + g.hop_plus;
+        }
+    }
+#pragma unroll
     for (int m = 0; m < kRngPerThread; ++m) {
-        PolarAttempt a = polar_attempt(st);
-        const uint64_t mask = __ballot(a.accept);
+        const uint64_t mask = __ballot((bits >> m) & 1u);
         if (lane == 0) cnt[m][w] = __popcll(mask);
-        st = g.hop_mult * st + g.hop_plus;
     }
     __syncthreads();
     if (tid == 0) {
@@ -193,43 +316,94 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
             }
     }
     __syncthreads();
-    st = st0;
+    // Pass 2: ranks come from the K1 accept flags, so an attempt's draws are
+    // recomputed only when one of its normals is stored (or it ends the call);
+    // every other attempt just jumps the state to the thread's next attempt.
+    uint64_t st = thread_first_state(g, sin->state, blockIdx.x, tid); // start of attempt m
     for (int m = 0; m < kRngPerThread; ++m) {
-        PolarAttempt a = polar_attempt(st);
-        const uint64_t mask = __ballot(a.accept);
-        if (a.accept) {
+        const bool acc = (bits >> m) & 1u;
+        const uint64_t mask = __ballot(acc);
+        // The wave's accepted attempts own the contiguous positions
+        // [q_first, q_first + 2*n_acc): locate q_first once per wave; a lane's
+        // position is then q_first + 2*below, at most one row wrap away when
+        // the run stays inside one array and rows hold >= 128 normals.
+        const long long rank0 = Ob + uniform(pre[m][w]); // scalar: the wave-level math below runs on the SALU
+        const int n_acc = __popcll(mask);
+        const uint64_t q_first = f + 2ull * (uint64_t)rank0;
+        const uint64_t q_end = q_first + 2ull * (uint64_t)n_acc; // exclusive
+        const StreamPos P0 = stream_pos(T, q_first);
+        const bool fast = n_acc > 0 && T.width[P0.sidx] >= 2 * 64 && q_end <= T.seg[P0.sidx + 1];
+        if (acc) {
             const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            const long long rank = Ob + pre[m][w] + below;
+            const long long rank = rank0 + below;
             if (rank < A) {
-                const uint64_t q0 = f + 2ull * (uint64_t)rank;
-                double *d0 = stream_dest(g, q0);
-                double *d1 = (q0 + 1 < g.Q) ? stream_dest(g, q0 + 1) : nullptr;
+                const uint64_t q0 = q_first + 2ull * (uint64_t)below;
+                StreamPos p0;
+                if (fast) {
+                    p0 = P0;
+                    p0.col += 2u * (uint32_t)below;
+                    if (p0.col >= T.width[P0.sidx]) {
+                        p0.col -= T.width[P0.sidx];
+                        p0.row++;
+                    }
+                } else {
+                    p0 = stream_pos(T, q0);
+                }
+                double *d0 = stream_dest(T, p0);
+                double *d1 = (q0 + 1 < g.Q) ? stream_dest(T, stream_next(T, p0)) : nullptr;
                 const bool last = (rank == A - 1);
                 if (d0 || d1 || last) {
-                    const double mult = sqrt(-2 * log(a.r2) / a.r2);
+                    uint64_t s4 = st;
+                    PolarAttempt a;
+                    if (g.debug_flags & 4) {
+                        a.x = (double)(uint32_t)st * 1e-10;
+                        a.y = 0.5;
+                        a.r2 = 0.5;
+                        s4 = st + 4;
+                    } else {
+                        a = polar_attempt(s4); // same draws K1 tested
+                    }
+                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * log(a.r2) / a.r2);
                     const double xm = a.x * mult;
                     const double ym = a.y * mult;
-                    if (d0) *d0 = ym * 1.0 + 0.0;
-                    if (d1) *d1 = xm * 1.0 + 0.0;
+                    const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;
+                    if (g.debug_flags & 2) {
+                        if (n0 == 1234.5) *d0 = n1; // keep the values alive
+                    } else if (d0 && d1 == d0 + 1 && ((uintptr_t)d0 & 15) == 0) {
+                        // adjacent and aligned (the common case): accepted lanes of a
+                        // wave then store one contiguous run of 16-B pairs
+                        *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
+                    } else {
+                        if (d0) *d0 = n0;
+                        if (d1) *d1 = n1;
+                    }
                     if (last) {
-                        sout->state = st; // state after this attempt's 4th output
+                        sout->state = s4; // state after this attempt's 4th output
                         sout->saved_flag = (int)((g.Q - f) & 1u);
                         sout->saved = xm;
                     }
                 }
             }
         }
-        st = g.hop_mult * st + g.hop_plus;
+        st = g.next_mult * st + g.next_plus;
     }
 }
 
-hipError_t launch_rng(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                      long long *offsets, int *err, int nblocks, hipStream_t st)
+hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, uint16_t *masks, int b0,
+                            int nb, int nb_total, hipStream_t st)
 {
-    hipLaunchKernelGGL(rng_count_kernel, dim3(nblocks), dim3(kRngThreads), 0, st, g, st_in, counts);
-    hipLaunchKernelGGL(rng_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, nblocks, st_in, g.Q, err);
-    hipLaunchKernelGGL(rng_generate_kernel, dim3(nblocks), dim3(kRngThreads), 0, st, g, st_in, st_out, offsets);
+    hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, masks, b0, nb_total);
+    return hipGetLastError();
+}
+
+hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
+                             long long *offsets, uint16_t *masks, int *err, int nb_total, int nb_scan, int own_b0,
+                             int own_b1, hipStream_t st)
+{
+    hipLaunchKernelGGL(rng_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, nb_scan, st_in, g.Q, err);
+    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, st_out, offsets,
+                       masks, counts, own_b0, own_b1);
     return hipGetLastError();
 }
 
@@ -248,10 +422,17 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
     const int lane = threadIdx.x & 63;
-    const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    // XCD-aware order (guide T1): blocks b and b+8 share an XCD, so hand each XCD
+    // a contiguous run of blocks; with strip-major tiles the row blocks that
+    // re-read the same noise rows then meet in one L2. gridDim.x % 8 == 0.
+    const int per_xcd = gridDim.x >> 3;
+    const int b = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    const int tile = uniform(b * 4 + (threadIdx.x >> 6));
     if (tile >= a.nstrips * nrowblk) return;
     const int s = tile / nrowblk;          // strip-major: neighbouring tiles share noise rows
-    const int j0 = (tile - s * nrowblk) * R;
+    int rb = tile - s * nrowblk;
+    if (a.heavy_first) rb = nrowblk - 1 - rb; // wide stencils (large j) start first: shorter tail
+    const int j0 = rb * R;
     const int Ny = a.Ny;
     const int nr = min(R, Ny - j0);
     const int col = s * kStrip + 2 * lane;
@@ -339,7 +520,7 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 {
     const int nrowblk = (a.Ny + R - 1) / R;
     const long long tiles = (long long)a.nstrips * nrowblk;
-    const unsigned blocks = (unsigned)((tiles + 3) / 4);
+    const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle
     if (!TABLE && a.nt_loads)
         hipLaunchKernelGGL((ypass_kernel<R, TABLE, true>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
     else
@@ -370,8 +551,9 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
     const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int Ny = a.Ny;
     if (tile >= a.nstrips * Ny) return;
-    const int j = tile / a.nstrips;
+    int j = tile / a.nstrips;
     const int s = tile - j * a.nstrips;
+    if (a.heavy_first) j = Ny - 1 - j;
     const int col = s * kStrip + 2 * lane;
 
     double f0[3], f1[3];

@@ -32,11 +32,21 @@ struct RngStateDev {
     double saved;
 };
 
+struct PcgJumpDev {
+    uint64_t mult, plus;
+};
+
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
-    uint64_t hop_mult, hop_plus; // jump over (kRngThreads-1)*4 outputs
+    uint64_t hop_mult, hop_plus;   // jump over (kRngThreads-1)*4 outputs (after an attempt's 4 draws)
+    uint64_t next_mult, next_plus; // jump over kRngThreads*4 outputs (attempt start to the next one)
+    const PcgJumpDev *jump_block;  // [nblocks]: jump over 4*4096*b outputs
+    const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*tid outputs
     int Nz_g, Pz, z0, z1, is_first, is_last;
+    uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
+    int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw
+    uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];
 };
@@ -60,13 +70,20 @@ struct SweepArgs {
     int do_corr, do_sra, comps_mask;
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
     int nt_loads;           // non-temporal loads for the coefficient stream
+    int heavy_first;        // schedule rows with the widest stencils first
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.
 hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_row, const double *tab,
                                 const int *tab_off, int Ny, int nstrips, int Nz_loc, hipStream_t st);
-hipError_t launch_rng(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                      long long *offsets, int *err, int nblocks, hipStream_t st);
+// K1 for blocks [b0, b0+nb) of nb_total (a z-strip rank counts its share only).
+hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, uint16_t *masks, int b0,
+                            int nb, int nb_total, hipStream_t st);
+// K2 + K3 once every block's count is present; blocks outside [own_b0, own_b1)
+// re-derive their accept flags.
+hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
+                             long long *offsets, uint16_t *masks, int *err, int nb_total, int nb_scan, int own_b0,
+                             int own_b1, hipStream_t st);
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st);
 hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
 // Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),

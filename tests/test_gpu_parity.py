@@ -230,3 +230,29 @@ def test_z_strips_in_process_match_single(world):
         cat = np.concatenate([s.field(k) for s in strips], axis=1)
         assert np.array_equal(cat, whole.field(k)), k
     assert all(s.rng_state() == whole.rng_state() for s in strips)
+
+
+def test_set_rng_state_discards_prefetched_noise():
+    # The next call's noise is generated ahead of time on a second stream; moving the
+    # stream must regenerate it (df.cpp:334-335 semantics: draws follow the state).
+    spec = (40, 70, 2, 8)
+    a = gpu_synth(*spec, seed=1)
+    a.filter(1e-8)
+    other = gpu_synth(*spec, seed=2)
+    st = other.rng_state()
+    a.set_rng_state(*st)
+    a.generate_white_noise()
+    c = gpu_synth(*spec, resume=st)  # its step 0 drew from st
+    for comp in range(3):
+        assert np.array_equal(a.noise(comp, "y"), c.noise(comp, "y"))
+    assert a.rng_state() == c.rng_state()
+    # and a no-op reset changes nothing
+    x = gpu_synth(*spec, seed=9)
+    y = gpu_synth(*spec, seed=9)
+    x.filter(1e-8)
+    y.filter(1e-8)
+    y.set_rng_state(*y.rng_state())
+    x.filter(1e-8)
+    y.filter(1e-8)
+    for k in FIELDS:
+        assert np.array_equal(x.field(k), y.field(k))

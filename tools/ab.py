@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""In-process A/B timing of library variants on one GPU (guide §5.4 rule 24).
+
+    python3 tools/ab.py --a "DFAMD_HEAVY_FIRST=0" --b "DFAMD_HEAVY_FIRST=1" [--config c3] [--mode packed]
+
+Each variant is a separate handle created with its env knobs set; the handles
+run interleaved rounds of K calls and the per-phase hipEvent times are reported
+as median over rounds.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
+import dfamd  # noqa: E402
+
+CFG = {"c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64)}
+
+
+def make(envspec, cfg, mode, rpw):
+    saved = {}
+    for kv in filter(None, envspec.split(",")):
+        k, v = kv.split("=")
+        saved[k] = os.environ.get(k)
+        os.environ[k] = v
+    Ny, Nz, a, b = CFG[cfg]
+    f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=a, N_max=b, seed=1, device=0,
+                            coeff_mode=mode, rows_per_wave=rpw)
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k)
+        else:
+            os.environ[k] = v
+    return f
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--a", default="")
+    ap.add_argument("--b", default="")
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--mode", default="packed")
+    ap.add_argument("--rpw-a", type=int, default=4)
+    ap.add_argument("--rpw-b", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--calls", type=int, default=10)
+    a = ap.parse_args()
+    hs = {"A": make(a.a, a.config, a.mode, a.rpw_a), "B": make(a.b, a.config, a.mode, a.rpw_b)}
+    rec = {k: {p: [] for p in ("rng_ms", "ypass_ms", "zpass_ms", "total_ms", "wall_ms")} for k in hs}
+    for f in hs.values():
+        for _ in range(3):
+            f.filter(1e-8)
+        f.sync()
+    for _ in range(a.rounds):
+        for k, f in hs.items():
+            f.set_profiling(True)
+            f.sync()
+            t0 = time.perf_counter()
+            for _ in range(a.calls):
+                f.filter(1e-8)
+            f.sync()
+            wall = (time.perf_counter() - t0) * 1e3 / a.calls
+            p = f.profile()
+            f.set_profiling(False)
+            p["wall_ms"] = wall * p["calls"]
+            for ph in rec[k]:
+                rec[k][ph].append(p[ph] / p["calls"])
+    out = {"A": a.a, "B": a.b, "config": a.config, "mode": a.mode}
+    for k in hs:
+        out[k + "_median_ms"] = {ph: round(statistics.median(v), 4) for ph, v in rec[k].items()}
+        out[k + "_min_ms"] = {ph: round(min(v), 4) for ph, v in rec[k].items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

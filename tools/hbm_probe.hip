@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <vector>
 #include <algorithm>
+#include <string>
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 
@@ -27,6 +28,16 @@ __global__ __launch_bounds__(256) void read_kernel(const dvec2 *__restrict__ p, 
     if (acc.x == 123.456 && acc.y == 654.321) *sink = acc.x; // keep loads alive
 }
 
+template <int W>
+__global__ __launch_bounds__(256) void write_kernel(double *__restrict__ p, size_t n_elems)
+{
+    size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_elems / W; i += stride) {
+        if (W == 2) reinterpret_cast<dvec2 *>(p)[i] = dvec2{1.0, 2.0};
+        else p[i] = 1.0;
+    }
+}
+
 __global__ __launch_bounds__(256) void copy_kernel(const dvec2 *__restrict__ a, dvec2 *__restrict__ b, size_t n)
 {
     size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -37,6 +48,23 @@ __global__ __launch_bounds__(256) void copy_kernel(const dvec2 *__restrict__ a, 
 
 int main(int argc, char **argv)
 {
+    if (argc > 1 && std::string(argv[1]) == "pmc") {
+        // One dispatch of each known-byte pattern for counter calibration (1 GiB each).
+        const size_t bytes = 1ull << 30, n = bytes / 16;
+        dvec2 *a;
+        double *sink;
+        CK(hipMalloc(&a, bytes));
+        CK(hipMalloc(&sink, 8));
+        CK(hipMemset(a, 0x3f, bytes));
+        CK(hipDeviceSynchronize());
+        hipLaunchKernelGGL(read_kernel<false>, dim3(8192), dim3(256), 0, 0, a, n, sink);
+        hipLaunchKernelGGL(read_kernel<true>, dim3(8192), dim3(256), 0, 0, a, n, sink);
+        hipLaunchKernelGGL(write_kernel<1>, dim3(8192), dim3(256), 0, 0, (double *)a, n * 2);
+        hipLaunchKernelGGL(write_kernel<2>, dim3(8192), dim3(256), 0, 0, (double *)a, n * 2);
+        CK(hipDeviceSynchronize());
+        printf("{\"pmc_probe_bytes\": %zu}\n", bytes);
+        return 0;
+    }
     size_t bytes = (argc > 1 ? strtoull(argv[1], 0, 10) : 8ull) << 30;
     size_t n = bytes / 16;
     dvec2 *a, *b;

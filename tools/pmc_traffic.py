@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--modes", default="packed,table")
     ap.add_argument("--json", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"))  # copy to profiles/
     a = ap.parse_args()
+    a.out, a.json = os.path.abspath(a.out), os.path.abspath(a.json)  # rocprofv3 runs from /tmp
     probe = [os.path.join(ROOT, "tools", "hbm_probe"), "pmc"]
     res = {"method": __doc__.strip().splitlines()[0], "config": a.config, "raw_kib": {}, "per_launch_bytes": {}}
     raw = {}
@@ -76,7 +77,8 @@ def main():
         for mode in a.modes.split(","):
             d = os.path.join(a.out, f"{mode}_{counter}")
             run_pmc(counter, d, [sys.executable, os.path.join(ROOT, "bench.py"), "--config", a.config,
-                                 "--coeff-mode", mode, "--steps", "3", "--warmup", "1", "--cpu-baseline", "off"])
+                                 "--coeff-mode", mode, "--steps", "3", "--warmup", "1", "--cpu-baseline", "off",
+                                 "--alt-modes", "off"])
             raw[(mode, counter)] = collapse(parse(d, counter))
     gib = float(1 << 30)
     pf = raw[("probe", "FETCH_SIZE")]

@@ -141,3 +141,38 @@ def test_c3_z_strips_in_process_match_single():
         cat = np.concatenate([s.field(k) for s in strips], axis=1)
         assert np.array_equal(cat, whole.field(k)), k
     assert all(s.rng_state() == whole.rng_state() for s in strips)
+
+
+def test_c5_full_size_sampled_rows():
+    """c5 (4096 x 4096, N 4-64): 85 GB of offset-packed coefficients on one GPU; the
+    Sigma(2N+1) = 1.7e9 offsets exceed nothing (64-bit on the device)."""
+    spec = dict(Ny=4096, Nz=4096, N_min=4, N_max=64)
+    seed = 5
+    g = dfamd.DigitalFilter(plane="synthetic", seed=seed, device=0, **spec)
+    m = RowModel(spec, seed)
+    rows = [0, 1, 819, 820, 2048, 4095]
+    ref = m.step(rows)
+    assert g.rng_state() == m.rng.state
+    for k in ("u", "v", "w"):
+        assert float(rel_err(g.field(k)[rows], ref[k]).max()) <= 1e-6, k
+    g.filter(1e-8)
+    ref = m.step(rows, 1e-8)
+    assert g.rng_state() == m.rng.state
+    for k in ("u", "v", "w", "T", "rho"):
+        assert float(rel_err(g.field(k)[rows], ref[k]).max()) <= 1e-6, k
+
+
+@pytest.mark.parametrize("spec", [dict(Ny=16, Nz=300, N_min=2, N_max=64),  # stencil far taller than the plane
+                                  dict(Ny=300, Nz=3, N_min=2, N_max=40),   # 3 columns, z-stencil >> Nz
+                                  dict(Ny=64, Nz=129, N_min=2, N_max=2)])  # one column past a strip
+def test_extreme_aspect_planes(spec):
+    seed = 11
+    g = dfamd.DigitalFilter(plane="synthetic", seed=seed, device=0, **spec)
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, seed=seed, **spec)
+    for dt in (None, 1e-8, 1e-8):
+        if dt is not None:
+            g.filter(dt)
+            o.filter(dt)
+        assert g.rng_state() == o.rng.state
+        for k in ("u", "v", "w", "T", "rho"):
+            assert float(rel_err(g.field(k), o.field(k)).max()) <= 1e-6, k

@@ -124,3 +124,40 @@ def test_host_only_handle_refuses_gpu_calls():
     f = host()
     with pytest.raises(dfamd.DFError, match="host-only"):
         f.filter(1e-8)
+
+
+def test_c_abi_rejects_bad_arguments():
+    import ctypes as C
+    L = dfamd.lib()
+    assert L.df_filter(None, 1e-8) == -1
+    assert b"null handle" in L.df_last_error()
+    f = host()
+    assert L.df_get_halfwidths(f._h, 3, 0, None) == -1
+    assert L.df_get_row(f._h, 99, (C.c_double * f.Ny)()) == -1
+    assert L.df_get_coeffs(f._h, 0, 0, (C.c_double * 4)(), 4) == -1  # too small
+    assert "too small" in L.df_last_error().decode()
+    cfg, keep = dfamd.make_config(device=-1, seed=1, coeff_mode="packed")
+    cfg.coeff_mode = 7
+    assert not L.df_create(C.byref(cfg))
+    assert b"coeff_mode" in L.df_last_error()
+    cfg, keep = dfamd.make_config(device=-1, seed=1, rows_per_wave=3)
+    assert not L.df_create(C.byref(cfg))
+    cfg, keep = dfamd.make_config(device=-1, seed=1, rank=2, world=2)
+    assert not L.df_create(C.byref(cfg))
+
+
+def test_reference_defaults_in_config():
+    import ctypes as C
+    cfg = dfamd._Cfg()
+    dfamd.lib().df_config_default(C.byref(cfg))
+    # df.cpp:7-10 hard-coded values
+    assert (cfg.d_i, cfg.rho_e, cfg.U_e, cfg.mu_e) == (0.0013, 0.044, 869.1, 7.1212e-6)
+    assert cfg.seed_from_random_device == 1 and cfg.plane == 0 and cfg.world == 1
+
+
+def test_d_i_from_config_changes_the_setup():
+    # the reference ignores DFConfig (df.cpp:7); here d_i scales the grid and length scales
+    a = host(plane="synthetic", Ny=32, Nz=8, N_min=2, N_max=8)
+    b = dfamd.DigitalFilter(device=-1, seed=1, plane="synthetic", Ny=32, Nz=8, N_min=2, N_max=8, d_i=0.002)
+    assert not np.array_equal(a.row("yc"), b.row("yc"))
+    assert np.allclose(b.row("yc") / a.row("yc"), 0.002 / 0.0013)

@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     p.add_argument("--coeff-mode", default="packed", choices=["packed", "table"])
-    p.add_argument("--rows-per-wave", type=int, default=4)
+    p.add_argument("--rows-per-wave", type=int, default=0)  # 0 = library default per mode
     p.add_argument("--dt", type=float, default=1e-8)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])

@@ -85,6 +85,7 @@ struct df_handle {
     int rows_per_wave = 8;
     int nt_loads = 1; // coefficient stream is read once per call: non-temporal (measured +6%)
     int heavy_first = 1;
+    int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
     CompDev c[3];
@@ -179,6 +180,8 @@ SweepArgs sweep_args(df_handle *h)
     a.comps_mask = 7;
     a.nt_loads = h->nt_loads;
     a.heavy_first = h->heavy_first;
+    a.yunroll = h->yunroll;
+    a.zunroll = h->zunroll;
     return a;
 }
 
@@ -450,10 +453,13 @@ int build(df_handle *h, const df_config_c *cfg)
     h->rank = cfg->rank;
     h->world = cfg->world < 1 ? 1 : cfg->world;
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
-    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : 4;
+    // measured best on MI355X (tools/ab.py same-handle A/B, profiles/r1): packed 2, table 4
+    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : (h->coeff_mode == DF_COEFF_TABLE ? 4 : 2);
     // tuning knobs for in-process A/B experiments (tools/ab.py); defaults are the measured best
     if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_HEAVY_FIRST")) h->heavy_first = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_YUNROLL")) h->yunroll = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_ZUNROLL")) h->zunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
     if (h->solo_strip) h->split_count = true;
@@ -804,7 +810,7 @@ void df_config_default(df_config_c *cfg)
     cfg->plane = DF_PLANE_NATIVE;
     cfg->coeff_mode = DF_COEFF_PACKED;
     cfg->world = 1;
-    cfg->rows_per_wave = 4;
+    cfg->rows_per_wave = 0;
 }
 
 df_handle *df_create(const df_config_c *cfg)
@@ -1090,6 +1096,24 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
 }
 
 long long df_stream_length(df_handle *h) { return valid(h) ? (long long)h->geom.Q : -1; }
+
+int df_set_tuning(df_handle *h, const char *key, int value)
+{
+    // Launch-shape knobs only: every setting produces bit-identical fields (tests/test_gpu_parity.py).
+    if (!h) return fail(DF_EINVAL, "null handle");
+    if (!key) return fail(DF_EINVAL, "null tuning key");
+    const std::string k(key);
+    if (k == "rows_per_wave") {
+        if (value != 1 && value != 2 && value != 4 && value != 8)
+            return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
+        h->rows_per_wave = value;
+    } else if (k == "nt_loads") h->nt_loads = value != 0;
+    else if (k == "heavy_first") h->heavy_first = value != 0;
+    else if (k == "yunroll") h->yunroll = value >= 4 ? 4 : 2;
+    else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
+    else return fail(DF_EINVAL, "unknown tuning key: " + k);
+    return DF_OK;
+}
 
 int df_set_profiling(df_handle *h, int on)
 {

@@ -416,7 +416,7 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 // i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
 // coalesced dwordx4 per (row, tap).
 
-template <int R, bool TABLE, bool NT>
+template <int R, bool TABLE, bool NT, int YU>
 __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 {
     const int c = blockIdx.y;
@@ -499,6 +499,14 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     const int bh = body_ok ? Nlo : thi;
     int t = tlo;
     for (; t < bl; ++t) predicated(t);
+    if (YU >= 4) {
+        for (; t + 3 <= bh; t += 4) {
+            body(t);
+            body(t + 1);
+            body(t + 2);
+            body(t + 3);
+        }
+    }
     for (; t + 1 <= bh; t += 2) {
         body(t);
         body(t + 1);
@@ -521,10 +529,17 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     const int nrowblk = (a.Ny + R - 1) / R;
     const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle
-    if (!TABLE && a.nt_loads)
-        hipLaunchKernelGGL((ypass_kernel<R, TABLE, true>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
-    else
-        hipLaunchKernelGGL((ypass_kernel<R, TABLE, false>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    if (!TABLE && a.nt_loads) {
+        if (a.yunroll >= 4)
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 4>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+        else
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    } else {
+        if (a.yunroll >= 4)
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 4>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+        else
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+    }
     return hipGetLastError();
 }
 
@@ -544,7 +559,7 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 // x[col+1+i]. With N even, pairs P_m = (x[col-N+2m], x[col-N+2m+1]) are 16-B
 // aligned: even tap -N+2m uses P_m, odd tap -N+2m+1 uses (P_m.y, P_{m+1}.x), so
 // one 16-B noise load serves two taps and the order i = -N..N is unchanged.
-template <bool TABLE, bool NT>
+template <bool TABLE, bool NT, int ZU>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -576,6 +591,31 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         double acc0 = 0.0, acc1 = 0.0;
         double2 P = xp[0];
         int m = 0;
+        if (ZU >= 4) {
+            for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
+                const double2 P1 = xp[m + 1], P2 = xp[m + 2], P3 = xp[m + 3], P4 = xp[m + 4];
+                double2 b[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) b[u] = coef(2 * m + u);
+                acc0 += b[0].x * P.x;
+                acc1 += b[0].y * P.y;
+                acc0 += b[1].x * P.y;
+                acc1 += b[1].y * P1.x;
+                acc0 += b[2].x * P1.x;
+                acc1 += b[2].y * P1.y;
+                acc0 += b[3].x * P1.y;
+                acc1 += b[3].y * P2.x;
+                acc0 += b[4].x * P2.x;
+                acc1 += b[4].y * P2.y;
+                acc0 += b[5].x * P2.y;
+                acc1 += b[5].y * P3.x;
+                acc0 += b[6].x * P3.x;
+                acc1 += b[6].y * P3.y;
+                acc0 += b[7].x * P3.y;
+                acc1 += b[7].y * P4.x;
+                P = P4;
+            }
+        }
         for (; m + 2 <= N; m += 2) {
             const double2 P1 = xp[m + 1], P2 = xp[m + 2];
             const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
@@ -650,9 +690,17 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
 {
     const long long tiles = (long long)a.nstrips * a.Ny;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
-    if (table) hipLaunchKernelGGL((zpass_kernel<true, false>), dim3(blocks), dim3(256), 0, st, a);
-    else if (a.nt_loads) hipLaunchKernelGGL((zpass_kernel<false, true>), dim3(blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((zpass_kernel<false, false>), dim3(blocks), dim3(256), 0, st, a);
+    const bool u4 = a.zunroll >= 4;
+    if (table) {
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<true, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+    } else if (a.nt_loads) {
+        if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<false, true, 2>), dim3(blocks), dim3(256), 0, st, a);
+    } else {
+        if (u4) hipLaunchKernelGGL((zpass_kernel<false, false, 4>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<false, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+    }
     return hipGetLastError();
 }
 

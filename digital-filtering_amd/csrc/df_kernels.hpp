@@ -71,6 +71,7 @@ struct SweepArgs {
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
     int nt_loads;           // non-temporal loads for the coefficient stream
     int heavy_first;        // schedule rows with the widest stencils first
+    int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.

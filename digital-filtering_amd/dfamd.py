@@ -93,6 +93,7 @@ def lib():
         "df_rms_count": (C.c_longlong, [H]),
         "df_get_vertices": (C.c_int, [H, C.c_void_p, C.c_void_p]),
         "df_set_profiling": (C.c_int, [H, C.c_int]),
+        "df_set_tuning": (C.c_int, [H, C.c_char_p, C.c_int]),
         "df_get_profile": (C.c_int, [H, C.POINTER(Profile)]),
         "df_sync": (C.c_int, [H]),
         "df_stream": (C.c_void_p, [H]),
@@ -127,7 +128,7 @@ def comm_unique_id():
 
 
 def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_mode="packed", device=0,
-                rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=4, rst_file=None, line_file=None,
+                rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=0, rst_file=None, line_file=None,
                 d_i=None, rho_e=None, U_e=None, mu_e=None, resume=None):
     """resume = (pcg state, saved_flag, saved): start the stream there instead of seeding."""
     cfg = _Cfg()
@@ -297,6 +298,9 @@ class DigitalFilter:
         return y, z
 
     # --- measurement
+    def set_tuning(self, key, value):
+        _check(lib().df_set_tuning(self._h, key.encode(), int(value)))
+
     def set_profiling(self, on):
         _check(lib().df_set_profiling(self._h, 1 if on else 0))
 

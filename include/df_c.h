@@ -154,6 +154,10 @@ long long df_rms_count(df_handle *h);
  * z per vertex column (Nz+1, global); y/z do not vary along the other axis. */
 int df_get_vertices(df_handle *h, double *y, double *z);
 
+/* Launch-shape tuning (extension; results are bit-identical for every setting):
+ * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4), "zunroll" (2,4). */
+int df_set_tuning(df_handle *h, const char *key, int value);
+
 /* Timing (hipEvents on the handle's stream). */
 int df_set_profiling(df_handle *h, int on);
 int df_get_profile(df_handle *h, df_profile *out);

@@ -200,6 +200,27 @@ def test_rows_per_wave_bitexact(rpw):
         assert np.array_equal(a[k], b[k]), (rpw, k)
 
 
+@pytest.mark.parametrize("mode", ["packed", "table"])
+def test_runtime_tuning_is_bitexact(mode):
+    # df_set_tuning flips launch shapes between calls; fields must not move by one bit
+    spec = (131, 260, 2, 16)
+    a = gpu_synth(*spec, seed=5, coeff_mode=mode)
+    b = gpu_synth(*spec, seed=5, coeff_mode=mode)
+    settings = [dict(rows_per_wave=1, zunroll=4, yunroll=4), dict(rows_per_wave=8, nt_loads=0, heavy_first=0),
+                dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_loads=1, heavy_first=1)]
+    for kw in settings:
+        for k, v in kw.items():
+            b.set_tuning(k, v)
+        a.filter(1e-8)
+        b.filter(1e-8)
+        for k in FIELDS:
+            assert np.array_equal(a.field(k), b.field(k)), (kw, k)
+    with pytest.raises(dfamd.DFError, match="unknown tuning"):
+        b.set_tuning("warp_size", 32)
+    with pytest.raises(dfamd.DFError, match="rows_per_wave"):
+        b.set_tuning("rows_per_wave", 3)
+
+
 def test_stage_api_matches_filter():
     spec = (96, 150, 2, 10)
     a = gpu_synth(*spec, seed=21)

@@ -6,6 +6,11 @@
 Each variant is a separate handle created with its env knobs set; the handles
 run interleaved rounds of K calls and the per-phase hipEvent times are reported
 as median over rounds.
+
+    python3 tools/ab.py --tune-a rows_per_wave=4 --tune-b rows_per_wave=2,zunroll=4
+
+--tune-* variants run on ONE handle (df_set_tuning between rounds), so both see
+the same allocations: separate handles differ by up to ~4% from page placement.
 """
 import argparse
 import json
@@ -44,12 +49,21 @@ def main():
     ap.add_argument("--b", default="")
     ap.add_argument("--config", default="c3")
     ap.add_argument("--mode", default="packed")
-    ap.add_argument("--rpw-a", type=int, default=4)
-    ap.add_argument("--rpw-b", type=int, default=4)
+    ap.add_argument("--rpw-a", type=int, default=0)
+    ap.add_argument("--rpw-b", type=int, default=0)
+    ap.add_argument("--tune-a", default=None)
+    ap.add_argument("--tune-b", default=None)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=10)
     a = ap.parse_args()
-    hs = {"A": make(a.a, a.config, a.mode, a.rpw_a), "B": make(a.b, a.config, a.mode, a.rpw_b)}
+    tune = None
+    if a.tune_a is not None or a.tune_b is not None:
+        one = make(a.a, a.config, a.mode, a.rpw_a)
+        hs = {"A": one, "B": one}
+        tune = {k: [(kv.split("=")[0], int(kv.split("=")[1])) for kv in filter(None, (v or "").split(","))]
+                for k, v in (("A", a.tune_a), ("B", a.tune_b))}
+    else:
+        hs = {"A": make(a.a, a.config, a.mode, a.rpw_a), "B": make(a.b, a.config, a.mode, a.rpw_b)}
     rec = {k: {p: [] for p in ("rng_ms", "ypass_ms", "zpass_ms", "total_ms", "wall_ms")} for k in hs}
     for f in hs.values():
         for _ in range(3):
@@ -57,6 +71,10 @@ def main():
         f.sync()
     for _ in range(a.rounds):
         for k, f in hs.items():
+            if tune is not None:
+                for key, val in tune[k]:
+                    f.set_tuning(key, val)
+                f.filter(1e-8)  # first call after a switch is not timed
             f.set_profiling(True)
             f.sync()
             t0 = time.perf_counter()
@@ -69,7 +87,7 @@ def main():
             p["wall_ms"] = wall * p["calls"]
             for ph in rec[k]:
                 rec[k][ph].append(p[ph] / p["calls"])
-    out = {"A": a.a, "B": a.b, "config": a.config, "mode": a.mode}
+    out = {"A": a.tune_a if tune else a.a, "B": a.tune_b if tune else a.b, "config": a.config, "mode": a.mode}
     for k in hs:
         out[k + "_median_ms"] = {ph: round(statistics.median(v), 4) for ph, v in rec[k].items()}
         out[k + "_min_ms"] = {ph: round(min(v), 4) for ph, v in rec[k].items()}

@@ -96,7 +96,7 @@ struct df_handle {
     int *counts = nullptr;
     long long *offsets = nullptr;
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
-    int *err_dev = nullptr;   // mapped host memory
+    int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped
     int *err_host = nullptr;
     int rng_blocks = 0;       // attempt blocks per call (4096 attempts each), same on every rank
     int rng_chunk = 0;        // blocks counted by each z-strip rank (split counting, SURVEY 8e option A)
@@ -664,8 +664,8 @@ int build(df_handle *h, const df_config_c *cfg)
         h->geom.jump_block = djb;
         h->geom.jump_thread = djt;
     }
-    HIP_OR(hipHostMalloc((void **)&h->err_host, sizeof(int), hipHostMallocMapped), DF_EHIP);
-    *h->err_host = 0;
+    HIP_OR(hipHostMalloc((void **)&h->err_host, 2 * sizeof(int), hipHostMallocMapped), DF_EHIP);
+    h->err_host[0] = h->err_host[1] = 0;
     HIP_OR(hipHostGetDevicePointer((void **)&h->err_dev, h->err_host, 0), DF_EHIP);
 
     uint64_t seed = cfg->seed;
@@ -796,6 +796,8 @@ extern "C" {
 int df_abi_version(void) { return DF_ABI_VERSION; }
 
 const char *df_last_error(void) { return g_err.c_str(); }
+
+size_t df_config_sizeof(void) { return sizeof(df_config_c); }
 
 void df_config_default(df_config_c *cfg)
 {
@@ -1141,7 +1143,28 @@ int df_sync(df_handle *h)
 {
     if (!valid_dev(h)) return DF_EINVAL;
     int rc = sync_all(h);
-    return rc ? rc : check_rng_error(h);
+    if (rc) return rc;
+    if ((rc = check_rng_error(h))) return rc;
+    if (const int bad = ((volatile int *)h->err_host)[1]) {
+        h->err_host[1] = 0;
+        return fail(DF_EINVAL, "df_gather_field: " + std::to_string(bad) + " out-of-range indices were skipped");
+    }
+    return DF_OK;
+}
+
+int df_gather_field(df_handle *h, int which, long long n, const long long *plane_cell, double *dst,
+                    const long long *dst_cell, long long dst_len, double beta)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    const double *src = df_device_field(h, which);
+    if (!src) return DF_EINVAL;
+    const long long nsrc = (long long)h->Ny * h->Nz_loc;
+    if (n < 0 || (n > 0 && !dst)) return fail(DF_EINVAL, "df_gather_field: bad count or null destination");
+    if (!plane_cell && n > nsrc) return fail(DF_EINVAL, "df_gather_field: n exceeds the plane without plane_cell");
+    if (!dst_cell && n > dst_len) return fail(DF_EINVAL, "df_gather_field: n exceeds dst_len without dst_cell");
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(launch_gather(src, nsrc, n, plane_cell, dst, dst_cell, dst_len, beta, h->err_dev + 1, h->stream), DF_EHIP);
+    return DF_OK;
 }
 
 void *df_stream(df_handle *h) { return valid_dev(h) ? (void *)h->stream : nullptr; }

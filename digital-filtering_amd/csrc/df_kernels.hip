@@ -803,6 +803,35 @@ __global__ void halo_unpack_kernel(SweepArgs a, const double *__restrict__ rl, c
     }
 }
 
+// ------------------------------------------------------------ K7 coupling handoff
+
+// dst[dst_cell[i]] = beta * dst[dst_cell[i]] + src[plane_cell[i]] (identity where an index array is null).
+__global__ void gather_kernel(const double *__restrict__ src, long long nsrc, long long n,
+                              const long long *__restrict__ pidx, double *__restrict__ dst,
+                              const long long *__restrict__ didx, long long ndst, double beta, int *bad)
+{
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const long long p = pidx ? pidx[i] : i;
+        const long long d = didx ? didx[i] : i;
+        if (p < 0 || p >= nsrc || d < 0 || d >= ndst) {
+            atomicAdd(bad, 1);
+            continue;
+        }
+        const double v = src[p];
+        dst[d] = beta == 0.0 ? v : beta * dst[d] + v;
+    }
+}
+
+hipError_t launch_gather(const double *src, long long nsrc, long long n, const long long *pidx, double *dst,
+                         const long long *didx, long long ndst, double beta, int *bad, hipStream_t st)
+{
+    if (n <= 0) return hipSuccess;
+    const long long want = (n + 255) / 256;
+    const int blocks = (int)(want < 4096 ? want : 4096);
+    hipLaunchKernelGGL(gather_kernel, dim3(blocks), dim3(256), 0, st, src, nsrc, n, pidx, dst, didx, ndst, beta, bad);
+    return hipGetLastError();
+}
+
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st)
 {
     hipLaunchKernelGGL(halo_pack_kernel, dim3(512), dim3(256), 0, st, a, send_l, send_r);

@@ -94,6 +94,8 @@ hipError_t launch_stage(const SweepArgs &a, int op, int comp, hipStream_t st);
 hipError_t launch_rms_add(const SweepArgs &a, double *acc, hipStream_t st);
 // plot_rms (df.cpp:615-621): out = sqrt(acc / count)
 hipError_t launch_rms_finish(const double *acc, double *out, size_t n, double count, hipStream_t st);
+hipError_t launch_gather(const double *src, long long nsrc, long long n, const long long *pidx, double *dst,
+                         const long long *didx, long long ndst, double beta, int *bad, hipStream_t st);
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st);
 hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st);
 

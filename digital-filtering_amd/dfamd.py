@@ -94,6 +94,8 @@ def lib():
         "df_get_vertices": (C.c_int, [H, C.c_void_p, C.c_void_p]),
         "df_set_profiling": (C.c_int, [H, C.c_int]),
         "df_set_tuning": (C.c_int, [H, C.c_char_p, C.c_int]),
+        "df_gather_field": (C.c_int, [H, C.c_int, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p, C.c_longlong,
+                                      C.c_double]),
         "df_get_profile": (C.c_int, [H, C.POINTER(Profile)]),
         "df_sync": (C.c_int, [H]),
         "df_stream": (C.c_void_p, [H]),
@@ -225,6 +227,10 @@ class DigitalFilter:
 
     def device_ptr(self, name):
         return lib().df_device_field(self._h, FIELDS[name])
+
+    def gather(self, name, dst, n, dst_len, plane_cell=None, dst_cell=None, beta=0.0):
+        """df_gather_field: device pointers (ints, e.g. torch data_ptr()) in, async on the library stream."""
+        _check(lib().df_gather_field(self._h, FIELDS[name], n, plane_cell, dst, dst_cell, dst_len, beta))
 
     def row(self, name):
         out = np.empty(self.Ny, dtype=np.float64)

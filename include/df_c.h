@@ -154,6 +154,15 @@ long long df_rms_count(df_handle *h);
  * z per vertex column (Nz+1, global); y/z do not vary along the other axis. */
 int df_get_vertices(df_handle *h, double *y, double *z);
 
+/* Device-side coupling handoff (the CFD inflow hook us3d_user.f90:51-130
+ * sets ghost-cell u = U + u'): for i < n, on the handle's stream after df_filter,
+ *     dst[dst_cell[i]] = beta * dst[dst_cell[i]] + field[plane_cell[i]]
+ * (beta == 0 assigns without reading dst). plane_cell / dst_cell are DEVICE int64
+ * arrays or NULL (identity); dst is device memory of dst_len doubles. No host sync:
+ * out-of-range indices are skipped and reported by the next df_sync. */
+int df_gather_field(df_handle *h, int which, long long n, const long long *plane_cell, double *dst,
+                    const long long *dst_cell, long long dst_len, double beta);
+
 /* Launch-shape tuning (extension; results are bit-identical for every setting):
  * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4), "zunroll" (2,4). */
 int df_set_tuning(df_handle *h, const char *key, int value);
@@ -171,6 +180,8 @@ int df_comm_unique_id(void *out, size_t len); /* RCCL unique id, len >= 128 */
 void df_destroy(df_handle *h);
 const char *df_last_error(void);
 int df_abi_version(void);
+/* sizeof(df_config_c) as compiled into the library (FFI layout check, e.g. the Fortran module). */
+size_t df_config_sizeof(void);
 
 #ifdef __cplusplus
 }

@@ -221,6 +221,34 @@ def test_runtime_tuning_is_bitexact(mode):
         b.set_tuning("rows_per_wave", 3)
 
 
+def test_gather_field_device_handoff():
+    import torch
+    f = gpu_synth(40, 33, 2, 6, seed=3)
+    f.filter(1e-8)
+    n = f.Ny * f.Nz_loc
+    u = torch.from_numpy(f.field("u").ravel()).cuda()
+    dst = torch.zeros(n, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    f.gather("u", dst.data_ptr(), n, n)  # identity copy, beta = 0
+    f.sync()
+    assert torch.equal(dst, u)
+    perm = torch.randperm(n, device="cuda")
+    base = torch.arange(n, dtype=torch.float64, device="cuda")
+    dst2 = base.clone()
+    torch.cuda.synchronize()
+    f.gather("u", dst2.data_ptr(), n, n, plane_cell=perm.data_ptr(), beta=1.0)  # dst += u[perm]
+    f.sync()
+    assert torch.equal(dst2, base + u[perm])
+    bad = torch.full((4,), n + 5, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    f.gather("u", dst.data_ptr(), 4, n, plane_cell=bad.data_ptr())
+    with pytest.raises(dfamd.DFError, match="out-of-range"):
+        f.sync()
+    f.sync()  # reported once
+    with pytest.raises(dfamd.DFError, match="dst_len"):
+        f.gather("u", dst.data_ptr(), n + 1, n, plane_cell=perm.data_ptr())
+
+
 def test_stage_api_matches_filter():
     spec = (96, 150, 2, 10)
     a = gpu_synth(*spec, seed=21)

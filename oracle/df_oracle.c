@@ -265,6 +265,32 @@ static void read_grid_synthetic(orc_df *df, int Ny, int Nz)
     }
 }
 
+static void read_grid_vertices(orc_df *df, int Ny, int Nz, const double *gy, const double *gz)
+{
+    /* read_grid() (df.cpp:71-118) on caller vertices instead of its placeholder grid */
+    df->Nz = Nz; df->Ny = Ny; df->n_cells = Nz * Ny;
+    size_t nv = (size_t)(Ny + 1) * (Nz + 1);
+    df->y = DALLOC(nv);
+    df->z = DALLOC(nv);
+    memcpy(df->y, gy, nv * sizeof(double));
+    memcpy(df->z, gz, nv * sizeof(double));
+    df->yc = DALLOC(df->n_cells); df->yc_d = DALLOC(df->n_cells);
+    df->dy = DALLOC(df->n_cells); df->dz = DALLOC(df->n_cells);
+    df->ydline = DALLOC(Ny); df->yline = DALLOC(Ny);
+    for (int j = 0; j < Ny; ++j) {
+        for (int k = 0; k < Nz; ++k) {
+            int idx = j * Nz + k;
+            df->dy[idx] = df->y[(j + 1) * (Nz + 1) + k] - df->y[j * (Nz + 1) + k];
+            df->dz[idx] = df->z[j * (Nz + 1) + k + 1] - df->z[j * (Nz + 1) + k];
+            df->yc[idx] = 0.25 * (df->y[j * (Nz + 1) + k] + df->y[(j + 1) * (Nz + 1) + k]
+                                  + df->y[j * (Nz + 1) + k + 1] + df->y[(j + 1) * (Nz + 1) + k + 1]);
+            df->yc_d[idx] = df->yc[idx] / df->d_i;
+        }
+        df->ydline[j] = df->yc_d[j * Nz];
+        df->yline[j] = df->yc[j * Nz];
+    }
+}
+
 /* ------------------------------------------------------ RST + line file */
 
 static int read_line_file(orc_df *df, const char *path)
@@ -397,7 +423,7 @@ static void calculate_filter_properties(orc_df *df, orc_field *F, const orc_cfg 
     F->Nz_max = 0; F->Ny_max = 0;
     for (int idx = 0; idx < n; ++idx) {
         int n_val;
-        if (cfg->plane == ORC_PLANE_NATIVE) {
+        if (cfg->plane != ORC_PLANE_SYNTHETIC) {
             Iz[idx] = F->Iz_inn + (F->Iz_out - F->Iz_inn) * 0.5 * (1 + tanh((df->yc[idx] / df->d_i - 0.2) / 0.03));
             double n_int = fmax(1.0, Iz[idx] / df->dz[idx]);
             n_val = 2 * (int)n_int;
@@ -420,7 +446,7 @@ static void calculate_filter_properties(orc_df *df, orc_field *F, const orc_cfg 
     b_size = 0;
     for (int idx = 0; idx < n; ++idx) {
         int n_val;
-        if (cfg->plane == ORC_PLANE_NATIVE) {
+        if (cfg->plane != ORC_PLANE_SYNTHETIC) {
             double Iy = 0.67 * Iz[idx];
             double n_int = fmax(1.0, Iy / df->dy[idx]);
             n_val = 2 * (int)n_int;
@@ -553,7 +579,12 @@ orc_df *orc_df_create(const orc_cfg *cfg, orc_rng *rng)
     df->rng = rng;
 
     if (cfg->plane == ORC_PLANE_NATIVE) read_grid_native(df);
-    else {
+    else if (cfg->plane == ORC_PLANE_GRID) {
+        if (cfg->Ny < 2 || cfg->Nz < 1 || !cfg->grid_y || !cfg->grid_z) {
+            set_err("bad grid plane spec", NULL); free(df); return NULL;
+        }
+        read_grid_vertices(df, cfg->Ny, cfg->Nz, cfg->grid_y, cfg->grid_z);
+    } else {
         if (cfg->Ny < 2 || cfg->Nz < 1 || cfg->N_min < 2 || cfg->N_max < cfg->N_min) {
             set_err("bad synthetic plane spec", NULL); free(df); return NULL;
         }

@@ -50,7 +50,7 @@ double orc_normal(orc_rng *r);
 void   orc_normals(orc_rng *r, double *out, size_t n);
 
 /* ---- the DIGITAL_FILTER object ---- */
-enum { ORC_PLANE_NATIVE = 0, ORC_PLANE_SYNTHETIC = 1 };
+enum { ORC_PLANE_NATIVE = 0, ORC_PLANE_SYNTHETIC = 1, ORC_PLANE_GRID = 2 };
 
 typedef struct {
     int plane;             /* ORC_PLANE_NATIVE: read_grid() df.cpp:71-118 */
@@ -58,6 +58,11 @@ typedef struct {
     int N_min, N_max;      /* synthetic half-width rule */
     const char *rst_file;  /* df.cpp:224 "../files/RST.dat" */
     const char *line_file; /* df.cpp:16  "../line.dat"      */
+    /* ORC_PLANE_GRID: the vertices read_grid() would read from grid_file (df.cpp:71-118 with
+     * its placeholder replaced): (Ny+1)*(Nz+1) y and z values, index j*(Nz+1)+k. Cell geometry
+     * follows df.cpp:104-116; dz is the cell's bottom edge z[j,k+1]-z[j,k] (the reference's
+     * placeholder grid has the constant 0.000133 there, df.cpp:108). */
+    const double *grid_y, *grid_z;
 } orc_cfg;
 
 typedef struct {

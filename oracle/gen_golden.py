@@ -121,6 +121,42 @@ def synth_fixture(name, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, dt2=None, nsteps2=
     json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=1)
 
 
+def grid_fixture(name, seed, Ny, Nz, dt, nsteps, full_steps=(), **grid_kw):
+    """Real-grid plane: caller vertices with per-cell dy, dz, yc, so the
+    half-widths vary per cell; setup, coefficients and the hot path are the reference's."""
+    gy, gz = O.warped_grid(Ny, Nz, **grid_kw)
+    with tempfile.TemporaryDirectory() as d:
+        vf = os.path.join(d, "vert.bin")
+        with open(vf, "wb") as f:
+            np.array([Ny, Nz], dtype=np.int32).tofile(f)
+            gy.tofile(f)
+            gz.tofile(f)
+        run("grid", RUN_ROOT, seed, vf, dt, nsteps, d)
+        meta = json.load(open(os.path.join(d, "meta.json")))
+        ny, nz = meta["Ny"], meta["Nz"]
+        rows = {r: np.fromfile(os.path.join(d, r + ".bin")) for r in ROWS}
+        Ns = {f"N{dn}_{c}": np.fromfile(os.path.join(d, f"N{dn}s_{c}.bin"), dtype=np.int32).reshape(ny, nz)
+              for c in "uvw" for dn in "yz"}
+        steps = [{k: np.fromfile(os.path.join(d, f"step{s}_{k}.bin")).reshape(ny, nz) for k in FIELDS}
+                 for s in range(nsteps + 1)]
+    assert any((Ns[k] != Ns[k][:, :1]).any() for k in Ns), "grid does not vary the half-width per cell"
+    rng = O.Rng(seed=seed)
+    O.Filter(rng=rng)
+    st, flag, saved = rng.state
+    arr = {"seed": seed, "Ny_in": Ny, "Nz_in": Nz, "Ny": ny, "Nz": nz, "dt": dt, "nsteps": nsteps,
+           "grid_y": gy, "grid_z": gz, "start_state": np.uint64(st), "start_saved_flag": flag,
+           "start_saved": saved, "full_steps": np.array(full_steps, dtype=np.int64)}
+    arr.update({f"row_{k}": v for k, v in rows.items()})
+    arr.update(Ns)
+    for s, stp in enumerate(steps):
+        for k in FIELDS:
+            arr[f"s{s}_{k}_stats"] = stats(stp[k])
+            if s in full_steps:
+                arr[f"s{s}_{k}"] = stp[k]
+    np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arr)
+    json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=1)
+
+
 def rms_fixture(name, seed, synth=None, sample_rows=None, csv_head=12):
     """The reference driver's own path: DIGITAL_FILTER df(config); df.get_rms() (cpp-main.cpp:12-17)."""
     with tempfile.TemporaryDirectory() as d:
@@ -155,6 +191,8 @@ def main():
     synth_fixture("ramp256_s1234", 1234, 256, 256, 4, 16, 1e-8, 2)
     # ragged plane: odd sizes, Nz smaller than the largest half-width
     synth_fixture("ragged_s7", 7, 37, 5, 2, 10, 1e-8, 2, full_steps=(0, 2), sample_rows=(0, 18, 36))
+    # real-grid plane: vertices vary along z, half-widths vary per cell; 2 strips, ragged
+    grid_fixture("grid_s3", 3, 60, 200, 1e-8, 2, full_steps=(0, 2))
     # the reference driver's get_rms() (500 steps at dt = 1e-5) on its native grid
     rms_fixture("rms_native_s42", 42)
     manifest = {

@@ -154,6 +154,46 @@ static void make_synthetic(DIGITAL_FILTER &df, int Ny, int Nz, int N_min, int N_
     df.apply_RST_scaling();
 }
 
+// Install caller vertices (a real inflow grid) in place of read_grid()'s placeholder
+// (df.cpp:71-118): per-cell dy, dz, yc exactly as df.cpp:104-116 derives them, with
+// dz taken from the vertices instead of the constant 0.000133 (df.cpp:108). Rows
+// (get_RST_in), integral scales (ctor values), half-widths and coefficients
+// (calculate_filter_properties) and step 0 are the reference's own code.
+static void make_grid(DIGITAL_FILTER &df, int Ny, int Nz, const std::vector<double> &gy,
+                      const std::vector<double> &gz)
+{
+    int n = Ny * Nz;
+    df.Ny = Ny; df.Nz = Nz; df.n_cells = n;
+    df.y = gy;
+    z = gz;
+    df.yc = Vector(n);
+    df.yc_d = Vector((size_t)n + Nz, 1e300); // sentinel row: get_RST_in's loop reads yc_d[Ny*Nz]
+    df.dy = Vector(n);
+    df.dz = Vector(n);
+    df.ydline = Vector(Ny);
+    df.yline = Vector(Ny);
+    for (int j = 0; j < Ny; ++j) {
+        for (int k = 0; k < Nz; ++k) {
+            int idx = j * Nz + k;
+            df.dy[idx] = df.y[(j + 1) * (Nz + 1) + k] - df.y[j * (Nz + 1) + k];
+            df.dz[idx] = z[j * (Nz + 1) + k + 1] - z[j * (Nz + 1) + k];
+            df.yc[idx] = 0.25 * (df.y[j * (Nz + 1) + k] + df.y[(j + 1) * (Nz + 1) + k]
+                                 + df.y[j * (Nz + 1) + k + 1] + df.y[(j + 1) * (Nz + 1) + k + 1]);
+            df.yc_d[idx] = df.yc[idx] / df.d_i;
+        }
+        df.ydline[j] = df.yc_d[j * Nz];
+        df.yline[j] = df.yc[j * Nz];
+    }
+    df.get_RST_in(); // truncates Ny to the RST profile's reach (df.cpp:280-304)
+    for (FilterField *F : {&df.u, &df.v, &df.w}) df.allocate_data_structures(*F);
+    df.rho_fluc = Vector(df.n_cells);
+    df.T_fluc = Vector(df.n_cells);
+    for (FilterField *F : {&df.u, &df.v, &df.w}) df.calculate_filter_properties(*F);
+    df.generate_white_noise();
+    for (FilterField *F : {&df.u, &df.v, &df.w}) df.filtering_sweeps(*F);
+    df.apply_RST_scaling();
+}
+
 static double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -217,6 +257,25 @@ int main(int argc, char **argv)
         int s = 1;
         for (; s <= nsteps; ++s) { df.filter(dt); dump_state(df, out, "step" + std::to_string(s)); }
         for (int t = 0; t < nsteps2; ++t, ++s) { df.filter(dt2); dump_state(df, out, "step" + std::to_string(s)); }
+        return 0;
+    }
+    if (mode == "grid") { // grid <root> <seed> <vertfile> <dt> <nsteps> <outdir>
+        FILE *f = fopen(argv[4], "rb");
+        if (!f) { perror(argv[4]); return 2; }
+        int dims[2];
+        if (fread(dims, 4, 2, f) != 2) return 2;
+        size_t nv = (size_t)(dims[0] + 1) * (dims[1] + 1);
+        std::vector<double> gy(nv), gz(nv);
+        if (fread(gy.data(), 8, nv, f) != nv || fread(gz.data(), 8, nv, f) != nv) return 2;
+        fclose(f);
+        double dt = strtod(argv[5], 0);
+        int nsteps = atoi(argv[6]);
+        std::string out = argv[7];
+        DIGITAL_FILTER df(cfg);
+        make_grid(df, dims[0], dims[1], gy, gz);
+        dump_setup(df, out);
+        dump_state(df, out, "step0");
+        for (int s = 1; s <= nsteps; ++s) { df.filter(dt); dump_state(df, out, "step" + std::to_string(s)); }
         return 0;
     }
     if (mode == "rms") { // rms <root> <seed> <outdir> [Ny Nz Nmin Nmax]: the reference driver's call (cpp-main.cpp:12-17)

@@ -105,6 +105,33 @@ def test_synthetic_planes_bitexact(golden, name):
     _check_case(f, g, dts)
 
 
+def test_grid_plane_bitexact(golden):
+    """Real-grid plane (per-cell half-widths): oracle vs the reference's own
+    calculate_filter_properties and hot path on the same vertices (gen_golden.grid_fixture)."""
+    g = golden("grid_s3.npz")
+    gy, gz = O.warped_grid(int(g["Ny_in"]), int(g["Nz_in"]))
+    assert np.array_equal(gy, g["grid_y"]) and np.array_equal(gz, g["grid_z"])
+    rng = O.Rng(seed=int(g["seed"]))
+    O.Filter(rng=rng)
+    assert rng.state == (int(g["start_state"]), int(g["start_saved_flag"]), float(g["start_saved"]))
+    f = O.Filter(plane=O.PLANE_GRID, Ny=int(g["Ny_in"]), Nz=int(g["Nz_in"]), grid_y=gy, grid_z=gz, rng=rng)
+    assert (f.Ny, f.Nz) == (int(g["Ny"]), int(g["Nz"]))
+    for k in ROWS8:
+        assert np.array_equal(f.row(k), g[f"row_{k}"]), k
+    for c, cn in enumerate("uvw"):
+        for d in "yz":
+            assert np.array_equal(f.halfwidths(c, d), g[f"N{d}_{cn}"]), (cn, d)
+    full = set(int(x) for x in g["full_steps"])
+    for s in range(int(g["nsteps"]) + 1):
+        if s:
+            f.filter(float(g["dt"]))
+        for k in FIELDS:
+            a = f.field(k)
+            assert np.array_equal(np.array([a.sum(), (a * a).sum(), np.abs(a).max()]), g[f"s{s}_{k}_stats"]), (s, k)
+            if s in full:
+                assert np.array_equal(a, g[f"s{s}_{k}"]), (s, k)
+
+
 def test_csv_writer_matches_reference(tmp_path, golden):
     g = golden("c1_s42.npz")
     rng = O.Rng(seed=42)

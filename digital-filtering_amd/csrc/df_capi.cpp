@@ -55,7 +55,8 @@ struct CompDev {
     double *ry[2] = {}, *rz[2] = {}; // double-buffered noise: set k%2 feeds call k
     double *By = nullptr, *Bz = nullptr;
     long long *byoff = nullptr, *bzoff = nullptr;
-    int *Ny_row = nullptr, *Nz_row = nullptr;
+    int *Ny_st = nullptr, *Nz_st = nullptr;     // tap range per (strip, row), [s*Ny + j]
+    int *Ny_cell = nullptr, *Nz_cell = nullptr; // per-cell N of this strip (grid planes only)
     double *filt_old = nullptr, *fluc = nullptr, *filt = nullptr;
     long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
     long long by_size = 0, bz_size = 0;   // reference offset-packed sizes (this strip's cells)
@@ -157,8 +158,10 @@ SweepArgs sweep_args(df_handle *h)
         a.Bz[c] = d.Bz;
         a.byoff[c] = d.byoff;
         a.bzoff[c] = d.bzoff;
-        a.Ny_row[c] = d.Ny_row;
-        a.Nz_row[c] = d.Nz_row;
+        a.Ny_st[c] = d.Ny_st;
+        a.Nz_st[c] = d.Nz_st;
+        a.Ny_cell[c] = d.Ny_cell;
+        a.Nz_cell[c] = d.Nz_cell;
         a.Nyp[c] = d.Nyp;
         a.Nzp[c] = d.Nzp;
         a.rz_pitch[c] = d.rz_pitch;
@@ -182,6 +185,7 @@ SweepArgs sweep_args(df_handle *h)
     a.heavy_first = h->heavy_first;
     a.yunroll = h->yunroll;
     a.zunroll = h->zunroll;
+    a.per_cell = h->setup.per_cell;
     return a;
 }
 
@@ -442,6 +446,18 @@ int build(df_handle *h, const df_config_c *cfg)
     h->spec.Nz = cfg->Nz;
     h->spec.N_min = cfg->N_min;
     h->spec.N_max = cfg->N_max;
+    if (cfg->plane == DF_PLANE_GRID) { // caller vertices, else the Tecplot grid_file (df.hpp:47)
+        if (cfg->grid_y && cfg->grid_z) {
+            if (cfg->Ny < 1 || cfg->Nz < 1) return fail(DF_EINVAL, "grid plane: Ny and Nz (cells) must be set with grid_y/grid_z");
+            const size_t nv = (size_t)(cfg->Ny + 1) * (cfg->Nz + 1);
+            h->spec.grid_y.assign(cfg->grid_y, cfg->grid_y + nv);
+            h->spec.grid_z.assign(cfg->grid_z, cfg->grid_z + nv);
+        } else if (cfg->grid_file) {
+            h->spec.grid_file = cfg->grid_file;
+        } else {
+            return fail(DF_EINVAL, "grid plane needs grid_y/grid_z vertex arrays or a grid_file");
+        }
+    }
     if (!cfg->vel_fluc_file || !cfg->line_file)
         return fail(DF_EINVAL, "vel_fluc_file (RST profile) and line_file (mean profile) are required");
     h->spec.rst_file = cfg->vel_fluc_file;
@@ -490,10 +506,17 @@ int build(df_handle *h, const df_config_c *cfg)
         d.Nyp = F.Ny_max;
         d.Nzp = F.Nz_max;
         d.rz_pitch = h->Pz + 2 * d.Nzp;
-        d.by_size = d.bz_size = 0;
+        d.by_size = d.bz_size = 0; // |by|, |bz| of the reference (df.cpp:151, 191) over this strip's cells
         for (int j = 0; j < Ny; ++j) {
-            d.by_size += (long long)h->Nz_loc * (2 * F.Ny_row[j] + 1);
-            d.bz_size += (long long)h->Nz_loc * (2 * F.Nz_row[j] + 1);
+            if (!s.per_cell) {
+                d.by_size += (long long)h->Nz_loc * (2 * F.Ny_row[j] + 1);
+                d.bz_size += (long long)h->Nz_loc * (2 * F.Nz_row[j] + 1);
+                continue;
+            }
+            for (int k = h->z0; k < h->z1; ++k) {
+                d.by_size += 2 * F.Ny_at(j, k) + 1;
+                d.bz_size += 2 * F.Nz_at(j, k) + 1;
+            }
         }
     }
 
@@ -563,10 +586,15 @@ int build(df_handle *h, const df_config_c *cfg)
     std::vector<double> tab_h;
     int Nmax_all = 0;
     for (auto &kv : s.coeffs) Nmax_all = std::max(Nmax_all, kv.first);
+    // Every N's half-vector padded with zeros to Nmax_all+1 entries, and a zero row at N = 0:
+    // per-cell reads past a lane's own N (up to its strip's N) then add exact zeros.
+    const size_t L = (size_t)Nmax_all + 1;
     tab_off_h.assign(Nmax_all + 1, 0);
+    tab_h.assign(L, 0.0); // row 0: all zeros (padding lanes)
     for (auto &kv : s.coeffs) {
         tab_off_h[kv.first] = (int)tab_h.size();
         tab_h.insert(tab_h.end(), kv.second.begin(), kv.second.end());
+        tab_h.resize(tab_h.size() + (L - kv.second.size()), 0.0);
     }
     int rc;
     if ((rc = dalloc_t(h, &h->tab, tab_h.size()))) return rc;
@@ -602,20 +630,47 @@ int build(df_handle *h, const df_config_c *cfg)
         }
         if ((rc = dalloc_t(h, &d.filt_old, n_loc))) return rc;
         if ((rc = dalloc_t(h, &d.fluc, n_loc))) return rc;
-        if ((rc = dalloc_t(h, &d.Ny_row, Ny))) return rc;
-        if ((rc = dalloc_t(h, &d.Nz_row, Ny))) return rc;
-        if ((rc = upload(h, d.Ny_row, F.Ny_row.data(), Ny))) return rc;
-        if ((rc = upload(h, d.Nz_row, F.Nz_row.data(), Ny))) return rc;
+        // tap range of each (strip, row): the largest N among the strip's cells of that row
+        std::vector<int> Nst[2];
+        for (int dir = 0; dir < 2; ++dir) {
+            Nst[dir].resize((size_t)h->nstrips * Ny);
+            for (int st = 0; st < h->nstrips; ++st)
+                for (int j = 0; j < Ny; ++j) {
+                    int m = dir ? F.Nz_row[j] : F.Ny_row[j];
+                    if (s.per_cell) {
+                        m = 0;
+                        const int k1 = std::min(h->z0 + (st + 1) * kStrip, h->z1);
+                        for (int k = h->z0 + st * kStrip; k < k1; ++k) m = std::max(m, dir ? F.Nz_at(j, k) : F.Ny_at(j, k));
+                    }
+                    Nst[dir][(size_t)st * Ny + j] = m;
+                }
+        }
+        if ((rc = dalloc_t(h, &d.Ny_st, Nst[0].size()))) return rc;
+        if ((rc = dalloc_t(h, &d.Nz_st, Nst[1].size()))) return rc;
+        if ((rc = upload(h, d.Ny_st, Nst[0].data(), Nst[0].size()))) return rc;
+        if ((rc = upload(h, d.Nz_st, Nst[1].data(), Nst[1].size()))) return rc;
+        if (s.per_cell) {
+            std::vector<int> nc[2];
+            for (int dir = 0; dir < 2; ++dir) {
+                nc[dir].resize(n_loc);
+                for (int j = 0; j < Ny; ++j)
+                    for (int kl = 0; kl < h->Nz_loc; ++kl)
+                        nc[dir][(size_t)j * h->Nz_loc + kl] = dir ? F.Nz_at(j, h->z0 + kl) : F.Ny_at(j, h->z0 + kl);
+            }
+            if ((rc = dalloc_t(h, &d.Ny_cell, n_loc))) return rc;
+            if ((rc = dalloc_t(h, &d.Nz_cell, n_loc))) return rc;
+            if ((rc = upload(h, d.Ny_cell, nc[0].data(), n_loc))) return rc;
+            if ((rc = upload(h, d.Nz_cell, nc[1].data(), n_loc))) return rc;
+        }
         if (h->coeff_mode == DF_COEFF_PACKED) {
             // strip-tap-major offsets, one block per (strip, row)
             for (int dir = 0; dir < 2; ++dir) {
-                const std::vector<int> &Nr = dir ? F.Nz_row : F.Ny_row;
                 std::vector<long long> off((size_t)h->nstrips * Ny);
                 long long run = 0;
                 for (int st = 0; st < h->nstrips; ++st)
                     for (int j = 0; j < Ny; ++j) {
                         off[(size_t)st * Ny + j] = run;
-                        run += (long long)(2 * Nr[j] + 1) * kStrip;
+                        run += (long long)(2 * Nst[dir][(size_t)st * Ny + j] + 1) * kStrip;
                     }
                 long long **doff = dir ? &d.bzoff : &d.byoff;
                 double **dB = dir ? &d.Bz : &d.By;
@@ -623,8 +678,8 @@ int build(df_handle *h, const df_config_c *cfg)
                 if ((rc = dalloc_t(h, doff, off.size()))) return rc;
                 if ((rc = upload(h, *doff, off.data(), off.size()))) return rc;
                 if ((rc = dalloc_t(h, dB, (size_t)run))) return rc;
-                HIP_OR(launch_expand_coeffs(*dB, *doff, dir ? d.Nz_row : d.Ny_row, h->tab, h->tab_off, Ny,
-                                            h->nstrips, h->Nz_loc, h->stream),
+                HIP_OR(launch_expand_coeffs(*dB, *doff, dir ? d.Nz_st : d.Ny_st, dir ? d.Nz_cell : d.Ny_cell,
+                                            h->tab, h->tab_off, Ny, h->nstrips, h->Nz_loc, h->stream),
                        DF_EHIP);
             }
         }
@@ -1018,21 +1073,23 @@ double df_get_scalar(df_handle *h, int which)
 int df_get_halfwidths(df_handle *h, int comp, int dir, int *out)
 {
     if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
-    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    const ComponentSetup &F = h->setup.comp[comp];
     for (int j = 0; j < h->Ny; ++j)
-        for (int k = 0; k < h->Nz_loc; ++k) out[(size_t)j * h->Nz_loc + k] = Nr[j];
+        for (int k = 0; k < h->Nz_loc; ++k)
+            out[(size_t)j * h->Nz_loc + k] = dir ? F.Nz_at(j, h->z0 + k) : F.Ny_at(j, h->z0 + k);
     return DF_OK;
 }
 
 int df_get_offsets(df_handle *h, int comp, int dir, int *out)
 {
     if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
-    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    const ComponentSetup &F = h->setup.comp[comp];
     long long b_size = 0; // df.cpp:151-152 / 191-192, over this strip's cells in row-major order
     for (int j = 0; j < h->Ny; ++j)
         for (int k = 0; k < h->Nz_loc; ++k) {
-            b_size += 2 * Nr[j] + 1;
-            out[(size_t)j * h->Nz_loc + k] = (int)(b_size - Nr[j] - 1);
+            const int N = dir ? F.Nz_at(j, h->z0 + k) : F.Ny_at(j, h->z0 + k);
+            b_size += 2 * N + 1;
+            out[(size_t)j * h->Nz_loc + k] = (int)(b_size - N - 1);
         }
     return DF_OK;
 }
@@ -1052,14 +1109,14 @@ int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n)
     if (!valid(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
     const long long need = dir ? h->c[comp].bz_size : h->c[comp].by_size;
     if (n < need) return fail(DF_EINVAL, "output too small for the packed coefficient vector");
-    const std::vector<int> &Nr = dir ? h->setup.comp[comp].Nz_row : h->setup.comp[comp].Ny_row;
+    const ComponentSetup &F = h->setup.comp[comp];
     long long pos = 0;
-    for (int j = 0; j < h->Ny; ++j) {
-        const std::vector<double> &half = h->setup.coeffs.at(Nr[j]);
-        const int N = Nr[j];
-        for (int k = 0; k < h->Nz_loc; ++k)
+    for (int j = 0; j < h->Ny; ++j)
+        for (int k = 0; k < h->Nz_loc; ++k) {
+            const int N = dir ? F.Nz_at(j, h->z0 + k) : F.Ny_at(j, h->z0 + k);
+            const std::vector<double> &half = h->setup.coeffs.at(N);
             for (int i = -N; i <= N; ++i) out[pos++] = half[i < 0 ? -i : i];
-    }
+        }
     return DF_OK;
 }
 
@@ -1252,6 +1309,28 @@ int df_get_vertices(df_handle *h, double *y, double *z)
     if (!valid(h)) return DF_EINVAL;
     if (y) std::copy(h->setup.y_vert.begin(), h->setup.y_vert.begin() + h->Ny + 1, y);
     if (z) std::copy(h->setup.z_vert.begin(), h->setup.z_vert.end(), z);
+    return DF_OK;
+}
+
+int df_get_grid(df_handle *h, double *y, double *z)
+{
+    if (!valid(h)) return DF_EINVAL;
+    const Setup &s = h->setup;
+    const int W = s.Nz + 1;
+    for (int j = 0; j <= s.Ny; ++j)
+        for (int k = 0; k < W; ++k) {
+            const size_t v = (size_t)j * W + k;
+            if (y) y[v] = s.yv.empty() ? s.y_vert[j] : s.yv[v];
+            if (z) z[v] = s.zv.empty() ? s.z_vert[k] : s.zv[v];
+        }
+    return DF_OK;
+}
+
+int df_plane_info(df_handle *h, int *plane, int *per_cell)
+{
+    if (!valid(h)) return DF_EINVAL;
+    if (plane) *plane = h->spec.kind;
+    if (per_cell) *per_cell = h->setup.per_cell ? 1 : 0;
     return DF_OK;
 }
 

@@ -32,31 +32,40 @@ template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
 
 // ------------------------------------------------------------------ K0 setup
 
+// Zero taps keep the reference's sum bit for bit: before a cell's first tap the sum
+// is +0 and +0 + (+-0) = +0; after its last tap x + (+-0) = x.
 __global__ __launch_bounds__(256) void expand_coeffs_kernel(double *__restrict__ B,
                                                             const long long *__restrict__ off,
-                                                            const int *__restrict__ N_row,
+                                                            const int *__restrict__ N_st,
+                                                            const int *__restrict__ N_cell,
                                                             const double *__restrict__ tab,
                                                             const int *__restrict__ tab_off, int Ny,
                                                             int Nz_loc)
 {
     const int sj = blockIdx.x; // s * Ny + j
     const int s = sj / Ny, j = sj - s * Ny;
-    const int N = N_row[j];
-    const double *h = tab + tab_off[N];
+    const int N = N_st[sj];
     double *dst = B + off[sj];
     const int total = (2 * N + 1) * kStrip;
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
         const int t = e / kStrip, cell = e - t * kStrip;
         const int i = t - N, ai = i < 0 ? -i : i;
-        dst[e] = (s * kStrip + cell < Nz_loc) ? h[ai] : 0.0;
+        const int k = s * kStrip + cell;
+        double v = 0.0;
+        if (k < Nz_loc) {
+            const int Nc = N_cell ? N_cell[(size_t)j * Nz_loc + k] : N;
+            if (ai <= Nc) v = tab[tab_off[Nc] + ai];
+        }
+        dst[e] = v;
     }
 }
 
-hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_row, const double *tab,
-                                const int *tab_off, int Ny, int nstrips, int Nz_loc, hipStream_t st)
+hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st, const int *N_cell,
+                                const double *tab, const int *tab_off, int Ny, int nstrips, int Nz_loc,
+                                hipStream_t st)
 {
-    hipLaunchKernelGGL(expand_coeffs_kernel, dim3((unsigned)nstrips * Ny), dim3(256), 0, st, B, off, N_row,
-                       tab, tab_off, Ny, Nz_loc);
+    hipLaunchKernelGGL(expand_coeffs_kernel, dim3((unsigned)nstrips * Ny), dim3(256), 0, st, B, off, N_st,
+                       N_cell, tab, tab_off, Ny, Nz_loc);
     return hipGetLastError();
 }
 
@@ -416,7 +425,7 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 // i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
 // coalesced dwordx4 per (row, tap).
 
-template <int R, bool TABLE, bool NT, int YU>
+template <int R, bool TABLE, bool NT, int YU, bool PC>
 __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 {
     const int c = blockIdx.y;
@@ -440,19 +449,26 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 
     int N[R];
     const double *bp[R];
-    const double *tb[R];
+    const double *tb[R], *tb1[R]; // table mode: half-vector of cell col (and col+1 when PC)
     int Nlo = 1 << 30, Nhi = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         N[r] = 0;
         bp[r] = nullptr;
-        tb[r] = nullptr;
+        tb[r] = tb1[r] = nullptr;
         if (r < nr) {
-            N[r] = a.Ny_row[c][j0 + r];
+            N[r] = a.Ny_st[c][(size_t)s * Ny + j0 + r];
             Nlo = min(Nlo, N[r]);
             Nhi = max(Nhi, N[r]);
-            if (TABLE) tb[r] = a.tab + a.tab_off[N[r]];
-            else bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + r] + (ptrdiff_t)(N[r] - r) * kStrip + 2 * lane;
+            if (TABLE && PC) { // per-lane N; the table is zero past each N (taps up to N_st)
+                const int *nc = a.Ny_cell[c] + (size_t)(j0 + r) * a.Nz_loc;
+                tb[r] = a.tab + a.tab_off[col < a.Nz_loc ? nc[col] : 0];
+                tb1[r] = a.tab + a.tab_off[col + 1 < a.Nz_loc ? nc[col + 1] : 0];
+            } else if (TABLE) {
+                tb[r] = a.tab + a.tab_off[N[r]];
+            } else {
+                bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + r] + (ptrdiff_t)(N[r] - r) * kStrip + 2 * lane;
+            }
         }
     }
     const double *np = a.ry[c] + (size_t)(j0 + a.Nyp[c]) * Pz + col;
@@ -463,8 +479,9 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 
     auto coef = [&](int r, int t) -> double2 {
         if (TABLE) {
-            const int i = t - r;
-            const double b = tb[r][i < 0 ? -i : i];
+            const int i = t - r, ai = i < 0 ? -i : i;
+            if (PC) return make_double2(tb[r][ai], tb1[r][ai]);
+            const double b = tb[r][ai];
             return make_double2(b, b);
         }
         return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
@@ -529,16 +546,19 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     const int nrowblk = (a.Ny + R - 1) / R;
     const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle
-    if (!TABLE && a.nt_loads) {
+    const dim3 grid(blocks, 3);
+    if (TABLE && a.per_cell)
+        hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
+    else if (!TABLE && a.nt_loads) {
         if (a.yunroll >= 4)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 4>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
         else
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
     } else {
         if (a.yunroll >= 4)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 4>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
         else
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
     }
     return hipGetLastError();
 }
@@ -559,7 +579,7 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 // x[col+1+i]. With N even, pairs P_m = (x[col-N+2m], x[col-N+2m+1]) are 16-B
 // aligned: even tap -N+2m uses P_m, odd tap -N+2m+1 uses (P_m.y, P_{m+1}.x), so
 // one 16-B noise load serves two taps and the order i = -N..N is unchanged.
-template <bool TABLE, bool NT, int ZU>
+template <bool TABLE, bool NT, int ZU, bool PC>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     const int lane = threadIdx.x & 63;
@@ -576,14 +596,22 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
     for (int c = 0; c < 3; ++c) {
         f0[c] = f1[c] = 0.0;
         if (!((a.comps_mask >> c) & 1)) continue;
-        const int N = a.Nz_row[c][j];
+        const int N = a.Nz_st[c][(size_t)s * Ny + j];
         const double2 *xp = reinterpret_cast<const double2 *>(a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col - N);
         const double *bp = TABLE ? nullptr : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + 2 * lane; // tap t = i + N
-        const double *tb = TABLE ? a.tab + a.tab_off[N] : nullptr;
+        const double *tb = nullptr, *tb1 = nullptr;
+        if (TABLE && PC) { // per-lane N; the table is zero past each N (taps up to N_st)
+            const int *nc = a.Nz_cell[c] + (size_t)j * a.Nz_loc;
+            tb = a.tab + a.tab_off[col < a.Nz_loc ? nc[col] : 0];
+            tb1 = a.tab + a.tab_off[col + 1 < a.Nz_loc ? nc[col + 1] : 0];
+        } else if (TABLE) {
+            tb = a.tab + a.tab_off[N];
+        }
         auto coef = [&](int t) -> double2 {
             if (TABLE) {
-                const int i = t - N;
-                const double v = tb[i < 0 ? -i : i];
+                const int i = t - N, ai = i < 0 ? -i : i;
+                if (PC) return make_double2(tb[ai], tb1[ai]);
+                const double v = tb[ai];
                 return make_double2(v, v);
             }
             return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
@@ -691,15 +719,17 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
     const long long tiles = (long long)a.nstrips * a.Ny;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
     const bool u4 = a.zunroll >= 4;
-    if (table) {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<true, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+    if (table && a.per_cell) {
+        hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
+    } else if (table) {
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), 0, st, a);
     } else if (a.nt_loads) {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<false, true, 2>), dim3(blocks), dim3(256), 0, st, a);
+        if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);
     } else {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<false, false, 4>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<false, false, 2>), dim3(blocks), dim3(256), 0, st, a);
+        if (u4) hipLaunchKernelGGL((zpass_kernel<false, false, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<false, false, 2, false>), dim3(blocks), dim3(256), 0, st, a);
     }
     return hipGetLastError();
 }

@@ -57,7 +57,9 @@ struct SweepArgs {
     double *rz[3];
     const double *By[3], *Bz[3];
     const long long *byoff[3], *bzoff[3]; // [s*Ny + j] element offsets
-    const int *Ny_row[3], *Nz_row[3];     // half-width per row
+    const int *Ny_st[3], *Nz_st[3];       // tap range per (strip, row): [s*Ny + j], max N over the strip's cells
+    const int *Ny_cell[3], *Nz_cell[3];   // per-cell N, [j*Nz_loc + k] (grid planes; table mode only)
+    int per_cell;                         // N varies within a strip: table mode reads lane N
     int Nyp[3], Nzp[3], rz_pitch[3];
     int Ny, Nz_loc, Pz, nstrips;
     // coefficient table (DF_COEFF_TABLE mode): half-vector of N at tab + tab_off[N]
@@ -75,8 +77,11 @@ struct SweepArgs {
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.
-hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_row, const double *tab,
-                                const int *tab_off, int Ny, int nstrips, int Nz_loc, hipStream_t st);
+// K0: strip-tap-major coefficients of one component and direction; taps beyond a cell's
+// own N (N_cell, or N_st when N_cell is null) are zero.
+hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st, const int *N_cell,
+                                const double *tab, const int *tab_off, int Ny, int nstrips, int Nz_loc,
+                                hipStream_t st);
 // K1 for blocks [b0, b0+nb) of nb_total (a z-strip rank counts its share only).
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, uint16_t *masks, int b0,
                             int nb, int nb_total, hipStream_t st);

@@ -7,7 +7,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cctype>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 
@@ -90,6 +92,53 @@ void grid_synthetic(const Flow &f, int Ny, int Nz, Setup &s)
     for (int j = 0; j <= Ny; ++j) s.y_vert[j] = j * hy;
 }
 
+// Tecplot BLOCK file as write_tecplot writes it (df.cpp:712-762): VARIABLES naming z and y
+// first, ZONE with I = Nz+1 and J = Ny+1, then I*J values of each variable in that order.
+bool read_tecplot_grid(const std::string &path, int &Ny, int &Nz, std::vector<double> &gy,
+                       std::vector<double> &gz, std::string &err)
+{
+    std::ifstream in(path);
+    if (!in) { err = "cannot open grid file " + path; return false; }
+    std::string line;
+    int I = -1, J = -1, yfirst = -1;
+    while (std::getline(in, line)) {
+        std::string up = line;
+        for (char &ch : up) ch = (char)std::toupper((unsigned char)ch);
+        if (up.find("VARIABLES") != std::string::npos) {
+            const size_t py = up.find("\"Y\""), pz = up.find("\"Z\"");
+            if (py == std::string::npos || pz == std::string::npos) { err = path + ": VARIABLES must name \"y\" and \"z\""; return false; }
+            yfirst = py < pz;
+        }
+        if (up.find("ZONE") != std::string::npos) {
+            auto num = [&](const char *key) {
+                size_t p = up.find(key);
+                return p == std::string::npos ? -1 : std::atoi(up.c_str() + p + std::strlen(key));
+            };
+            I = num("I=");
+            J = num("J=");
+            break;
+        }
+    }
+    if (yfirst < 0 || I < 2 || J < 3) { err = path + ": needs VARIABLES and ZONE I=(Nz+1) J=(Ny+1) headers"; return false; }
+    const size_t n = (size_t)I * J;
+    std::vector<double> a(n), b(n);
+    size_t got = 0;
+    std::string tok;
+    while (got < 2 * n && in >> tok) {
+        char *end = nullptr;
+        const double v = std::strtod(tok.c_str(), &end);
+        if (end == tok.c_str()) continue; // VARLOCATION / DT lines
+        (got < n ? a[got] : b[got - n]) = v;
+        ++got;
+    }
+    if (got < 2 * n) { err = path + ": fewer values than 2*I*J"; return false; }
+    Nz = I - 1;
+    Ny = J - 1;
+    gy = yfirst ? a : b;
+    gz = yfirst ? b : a;
+    return true;
+}
+
 void cell_geometry(const Flow &f, Setup &s)
 {
     const int Ny = s.Ny, Nz = s.Nz;
@@ -131,7 +180,50 @@ void cell_coefficients(int N, double *half)
 
 bool build_setup(const Flow &f, const PlaneSpec &spec, Setup &s, std::string &err)
 {
-    if (spec.kind == kPlaneNative) {
+    // per-cell geometry of a grid plane (df.cpp:104-116 on caller vertices)
+    std::vector<double> cyc, cdy, cdz;
+    if (spec.kind == kPlaneGrid) {
+        int Ny = spec.Ny, Nz = spec.Nz;
+        std::vector<double> gy = spec.grid_y, gz = spec.grid_z;
+        if (gy.empty() && !spec.grid_file.empty()) {
+            if (!read_tecplot_grid(spec.grid_file, Ny, Nz, gy, gz, err)) return false;
+        }
+        if (Ny < 2 || Nz < 1 || gy.size() != (size_t)(Ny + 1) * (Nz + 1) || gz.size() != gy.size()) {
+            err = "grid plane needs Ny >= 2, Nz >= 1 and (Ny+1)*(Nz+1) y and z vertices (or a grid_file)";
+            return false;
+        }
+        s.Ny = Ny;
+        s.Nz = Nz;
+        const size_t n = (size_t)Ny * Nz;
+        cyc.resize(n);
+        cdy.resize(n);
+        cdz.resize(n);
+        for (int j = 0; j < Ny; ++j)
+            for (int k = 0; k < Nz; ++k) {
+                const size_t idx = (size_t)j * Nz + k, v00 = (size_t)j * (Nz + 1) + k, v10 = v00 + Nz + 1;
+                cdy[idx] = gy[v10] - gy[v00];                              // df.cpp:107
+                cdz[idx] = gz[v00 + 1] - gz[v00];                          // bottom edge (df.cpp:108 placeholder)
+                cyc[idx] = 0.25 * (gy[v00] + gy[v10] + gy[v00 + 1] + gy[v10 + 1]); // df.cpp:109-112
+                if (!(cdy[idx] > 0) || !(cdz[idx] > 0)) {
+                    err = "grid plane: vertices must increase in j (y) and k (z) at every cell";
+                    return false;
+                }
+            }
+        s.yv = std::move(gy);
+        s.zv = std::move(gz);
+        // rows (ydline, yline, dy per row) come from column 0 as in df.cpp:116
+        s.y_vert.resize(Ny + 1);
+        for (int j = 0; j <= Ny; ++j) s.y_vert[j] = s.yv[(size_t)j * (Nz + 1)];
+        s.z_vert.assign(s.zv.begin(), s.zv.begin() + Nz + 1);
+        s.yc.resize(Ny);
+        s.yc_d.resize(Ny);
+        s.dy.resize(Ny);
+        for (int j = 0; j < Ny; ++j) {
+            s.yc[j] = cyc[(size_t)j * Nz];
+            s.yc_d[j] = s.yc[j] / f.d_i;
+            s.dy[j] = cdy[(size_t)j * Nz];
+        }
+    } else if (spec.kind == kPlaneNative) {
         grid_native(f, s);
     } else if (spec.kind == kPlaneSynthetic) {
         if (spec.Ny < 2 || spec.Nz < 1 || spec.N_min < 2 || spec.N_max < spec.N_min) {
@@ -143,7 +235,7 @@ bool build_setup(const Flow &f, const PlaneSpec &spec, Setup &s, std::string &er
         err = "unknown plane kind";
         return false;
     }
-    cell_geometry(f, s);
+    if (spec.kind != kPlaneGrid) cell_geometry(f, s);
 
     // ---- get_RST_in (df.cpp:220-330)
     std::vector<std::vector<double>> rst;
@@ -162,6 +254,8 @@ bool build_setup(const Flow &f, const PlaneSpec &spec, Setup &s, std::string &er
     while (new_Ny < s.Ny && s.yc_d[new_Ny] <= yin_d[N_in - 1]) new_Ny++;
     if (new_Ny < 2) { err = "RST profile covers fewer than two grid rows"; return false; }
     s.Ny = new_Ny;
+    if (!s.yv.empty()) s.yv.resize((size_t)(s.Ny + 1) * (s.Nz + 1)); // df.cpp:297 keeps the first rows
+    if (!s.zv.empty()) s.zv.resize((size_t)(s.Ny + 1) * (s.Nz + 1));
     s.y_vert.resize(s.Ny + 1);
     s.yc.resize(s.Ny);
     s.yc_d.resize(s.Ny);
@@ -212,10 +306,48 @@ bool build_setup(const Flow &f, const PlaneSpec &spec, Setup &s, std::string &er
     u.Iz_out = 0.4 * f.d_i; u.Iz_inn = 150 * s.d_v; u.Lt = 0.8 * f.d_i / f.U_e;
     v.Iz_out = 0.3 * f.d_i; v.Iz_inn = 75 * s.d_v;  v.Lt = 0.3 * f.d_i / f.U_e;
     w.Iz_out = 0.4 * f.d_i; w.Iz_inn = 150 * s.d_v; w.Lt = 0.3 * f.d_i / f.U_e;
+    const bool grid = spec.kind == kPlaneGrid;
+    s.per_cell = false;
     for (ComponentSetup &F : s.comp) {
         F.Ny_row.resize(s.Ny);
         F.Nz_row.resize(s.Ny);
+        F.Nz_cols = s.Nz;
         F.Ny_max = F.Nz_max = 0;
+        if (grid) { // df.cpp:144-149, 185-190 per cell
+            const size_t n = (size_t)s.Ny * s.Nz;
+            F.Ny_cell.resize(n);
+            F.Nz_cell.resize(n);
+            for (int j = 0; j < s.Ny; ++j) {
+                int ry = 0, rz = 0;
+                for (int k = 0; k < s.Nz; ++k) {
+                    const size_t idx = (size_t)j * s.Nz + k;
+                    const double Iz = F.Iz_inn + (F.Iz_out - F.Iz_inn) * 0.5 * (1 + std::tanh((cyc[idx] / f.d_i - 0.2) / 0.03));
+                    const int nz = 2 * (int)std::max(1.0, Iz / cdz[idx]);
+                    const double Iy = 0.67 * Iz;
+                    const int ny = 2 * (int)std::max(1.0, Iy / cdy[idx]);
+                    F.Nz_cell[idx] = nz;
+                    F.Ny_cell[idx] = ny;
+                    if (k && (nz != F.Nz_cell[idx - 1] || ny != F.Ny_cell[idx - 1])) s.per_cell = true;
+                    ry = std::max(ry, ny);
+                    rz = std::max(rz, nz);
+                    if (!s.coeffs.count(ny)) {
+                        std::vector<double> hv(ny + 1);
+                        cell_coefficients(ny, hv.data());
+                        s.coeffs.emplace(ny, std::move(hv));
+                    }
+                    if (!s.coeffs.count(nz)) {
+                        std::vector<double> hv(nz + 1);
+                        cell_coefficients(nz, hv.data());
+                        s.coeffs.emplace(nz, std::move(hv));
+                    }
+                }
+                F.Ny_row[j] = ry;
+                F.Nz_row[j] = rz;
+                F.Ny_max = std::max(F.Ny_max, ry);
+                F.Nz_max = std::max(F.Nz_max, rz);
+            }
+            continue;
+        }
         for (int j = 0; j < s.Ny; ++j) {
             int nz, ny;
             if (spec.kind == kPlaneNative) {
@@ -241,6 +373,11 @@ bool build_setup(const Flow &f, const PlaneSpec &spec, Setup &s, std::string &er
             }
         }
     }
+    if (grid && !s.per_cell) // row-uniform grid: the per-row representation is exact
+        for (ComponentSetup &F : s.comp) {
+            F.Ny_cell.clear();
+            F.Nz_cell.clear();
+        }
     return true;
 }
 
@@ -250,12 +387,18 @@ bool write_csv(const Setup &s, const std::string &path, const double *u, const d
     FILE *f = std::fopen(path.c_str(), "w");
     if (!f) { err = "cannot open " + path + " for writing"; return false; }
     std::fputs("z,y,u_fluc,v_fluc,w_fluc,T_fluc,rho_fluc\n", f);
+    const int W = s.Nz + 1;
     for (int j = 0; j < s.Ny; ++j) {
         const double y0 = s.y_vert[j], y1 = s.y_vert[j + 1];
-        const double yc = 0.25 * (y0 + y0 + y1 + y1); // n00, n01, n10, n11 (df.cpp:779-785)
+        double yc = 0.25 * (y0 + y0 + y1 + y1); // n00, n01, n10, n11 (df.cpp:779-785)
         for (int kl = 0; kl < nz; ++kl) {
             const int k = z0 + kl;
-            const double zc = 0.25 * (s.z_vert[k] + s.z_vert[k + 1] + s.z_vert[k] + s.z_vert[k + 1]);
+            double zc = 0.25 * (s.z_vert[k] + s.z_vert[k + 1] + s.z_vert[k] + s.z_vert[k + 1]);
+            if (!s.yv.empty()) { // grid plane: the cell's own four vertices
+                const size_t n00 = (size_t)j * W + k, n01 = n00 + 1, n10 = n00 + W, n11 = n10 + 1;
+                yc = 0.25 * (s.yv[n00] + s.yv[n01] + s.yv[n10] + s.yv[n11]);
+                zc = 0.25 * (s.zv[n00] + s.zv[n01] + s.zv[n10] + s.zv[n11]);
+            }
             const size_t c = (size_t)j * nz + kl;
             std::fprintf(f, "%.15f,%.15f,%.15f,%.15f,%.15f,%.15f,%.15f\n", zc, yc, u[c], v[c], w[c], T[c], rho[c]);
         }

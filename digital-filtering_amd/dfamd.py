@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libdfamd.so")
 DATA = os.path.join(HERE, "data")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "df_c.h")
 
-PLANE = {"native": 0, "synthetic": 1}
+PLANE = {"native": 0, "synthetic": 1, "grid": 2}
 COEFF = {"packed": 0, "table": 1}
 FIELDS = {"u": 0, "v": 1, "w": 2, "T": 3, "rho": 4, "filt_old_u": 5, "filt_old_v": 6, "filt_old_w": 7,
           "filt_u": 8, "filt_v": 9, "filt_w": 10}
@@ -37,6 +37,7 @@ class _Cfg(C.Structure):
         ("coeff_mode", C.c_int), ("csv_path", C.c_char_p), ("device", C.c_int),
         ("rank", C.c_int), ("world", C.c_int), ("comm_id", C.c_void_p), ("rows_per_wave", C.c_int),
         ("rng_resume", C.c_int), ("rng_saved_flag", C.c_int), ("rng_state", C.c_uint64), ("rng_saved", C.c_double),
+        ("grid_y", C.c_void_p), ("grid_z", C.c_void_p),
     ]
 
 
@@ -92,6 +93,8 @@ def lib():
         "df_rms_get": (C.c_int, [H, C.c_int, C.c_void_p]),
         "df_rms_count": (C.c_longlong, [H]),
         "df_get_vertices": (C.c_int, [H, C.c_void_p, C.c_void_p]),
+        "df_get_grid": (C.c_int, [H, C.c_void_p, C.c_void_p]),
+        "df_plane_info": (C.c_int, [H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "df_set_profiling": (C.c_int, [H, C.c_int]),
         "df_set_tuning": (C.c_int, [H, C.c_char_p, C.c_int]),
         "df_gather_field": (C.c_int, [H, C.c_int, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p, C.c_longlong,
@@ -131,8 +134,9 @@ def comm_unique_id():
 
 def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_mode="packed", device=0,
                 rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=0, rst_file=None, line_file=None,
-                d_i=None, rho_e=None, U_e=None, mu_e=None, resume=None):
-    """resume = (pcg state, saved_flag, saved): start the stream there instead of seeding."""
+                d_i=None, rho_e=None, U_e=None, mu_e=None, resume=None, grid_y=None, grid_z=None, grid_file=None):
+    """resume = (pcg state, saved_flag, saved): start the stream there instead of seeding.
+    plane="grid": grid_y / grid_z vertex arrays of shape (Ny+1, Nz+1) (Ny, Nz cells), or grid_file."""
     cfg = _Cfg()
     lib().df_config_default(C.byref(cfg))
     keep = []
@@ -154,6 +158,17 @@ def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_m
         cfg.seed = seed
     cfg.plane = PLANE[plane]
     cfg.Ny, cfg.Nz, cfg.N_min, cfg.N_max = Ny, Nz, N_min, N_max
+    if grid_y is not None:
+        gy = np.ascontiguousarray(grid_y, dtype=np.float64)
+        gz = np.ascontiguousarray(grid_z, dtype=np.float64)
+        if gy.ndim == 2 and not (Ny or Nz):
+            cfg.Ny, cfg.Nz = gy.shape[0] - 1, gy.shape[1] - 1
+        if gy.size != (cfg.Ny + 1) * (cfg.Nz + 1) or gz.size != gy.size:
+            raise DFError("grid_y/grid_z must hold (Ny+1)*(Nz+1) vertices")
+        keep += [gy, gz]
+        cfg.grid_y, cfg.grid_z = gy.ctypes.data, gz.ctypes.data
+    if grid_file:
+        cfg.grid_file = cstr(grid_file)
     cfg.coeff_mode = COEFF[coeff_mode]
     cfg.csv_path = cstr(csv_path) if csv_path else None
     cfg.device, cfg.rank, cfg.world = device, rank, world
@@ -302,6 +317,18 @@ class DigitalFilter:
         z = np.empty(self.Nz + 1)
         _check(lib().df_get_vertices(self._h, y.ctypes.data, z.ctypes.data))
         return y, z
+
+    def grid(self):
+        """All vertices: (y, z), each (Ny+1, Nz+1)."""
+        y = np.empty((self.Ny + 1, self.Nz + 1))
+        z = np.empty_like(y)
+        _check(lib().df_get_grid(self._h, y.ctypes.data, z.ctypes.data))
+        return y, z
+
+    def plane_info(self):
+        p, pc = C.c_int(), C.c_int()
+        _check(lib().df_plane_info(self._h, C.byref(p), C.byref(pc)))
+        return p.value, bool(pc.value)
 
     # --- measurement
     def set_tuning(self, key, value):

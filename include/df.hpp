@@ -55,14 +55,15 @@ struct FilterField { // df.hpp:24-34
 struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     double d_i = 0.0013, rho_e = 0.044, U_e = 869.1, mu_e = 7.1212e-6;
     int vel_file_offset = 0, vel_file_N_values = 0;
-    std::string grid_file;                                   // unused (no grid reader, as in the reference)
+    std::string grid_file;                                   // DF_PLANE_GRID: Tecplot BLOCK grid (write_tecplot layout)
     std::string vel_fluc_file = DF_DATA_DIR "/RST.dat";      // RST profile (reference: ../files/RST.dat)
     // ---- extensions
     std::string line_file = DF_DATA_DIR "/line.dat";         // mean profile (reference: ../line.dat)
     std::uint64_t seed = 0;
     bool seed_from_random_device = true;                     // df.cpp:334
     int plane = DF_PLANE_NATIVE;                             // DF_PLANE_SYNTHETIC: Ny x Nz, N in [N_min, N_max]
-    int Ny = 0, Nz = 0, N_min = 0, N_max = 0;
+    int Ny = 0, Nz = 0, N_min = 0, N_max = 0;                // DF_PLANE_GRID: Ny x Nz cells of grid_y/grid_z
+    Vector grid_y, grid_z;                                   // DF_PLANE_GRID vertices, (Ny+1)*(Nz+1), j*(Nz+1)+k
     int coeff_mode = DF_COEFF_PACKED;
     std::string csv_path;                                    // e.g. "../files/cpp_vel_fluc.csv" (df.cpp:466)
     std::string rms_csv_path = "../files/cpp_vel_fluc_rms.csv"; // df.cpp:623
@@ -87,7 +88,7 @@ class DIGITAL_FILTER {
     Vector R11, R21, R22, R33;
     int rms_counter = 0;
     double dt = 0.0;
-    Vector yv_, zv_;           // vertex y per row, z per column
+    Vector y, z;               // vertices of this strip, (Ny+1)*(Nz+1), index j*(Nz+1)+k (df.hpp:61)
     Vector Us, Ts, rhos, Ps, Ms;
     double d_i = 0, d_v = 0, u_tau = 0, tau_w = 0;
     Vector T_rms, rho_rms;
@@ -165,7 +166,9 @@ class DIGITAL_FILTER {
         c.mu_e = config.mu_e;
         c.vel_file_offset = config.vel_file_offset;
         c.vel_file_N_values = config.vel_file_N_values;
-        c.grid_file = config.grid_file.c_str();
+        c.grid_file = config.grid_file.empty() ? nullptr : config.grid_file.c_str();
+        c.grid_y = config.grid_y.empty() ? nullptr : config.grid_y.data();
+        c.grid_z = config.grid_z.empty() ? nullptr : config.grid_z.data();
         c.vel_fluc_file = config.vel_fluc_file.c_str();
         c.line_file = config.line_file.c_str();
         c.seed = config.seed;
@@ -205,10 +208,17 @@ class DIGITAL_FILTER {
         rhos = row(DF_ROW_RHOS);
         Ps = row(DF_ROW_PS);
         Ms = row(DF_ROW_MS);
-        yv_.resize(Ny + 1);
-        zv_.resize(nz + 1);
-        check(df_get_vertices(h_, yv_.data(), zv_.data()));
-        zv_.assign(zv_.begin() + z0, zv_.begin() + z1 + 1);
+        {
+            Vector gy((size_t)(Ny + 1) * (nz + 1)), gz(gy.size());
+            check(df_get_grid(h_, gy.data(), gz.data()));
+            y.resize((size_t)(Ny + 1) * (Nz + 1));
+            z.resize(y.size());
+            for (int j = 0; j <= Ny; ++j)
+                for (int k = 0; k <= Nz; ++k) {
+                    y[(size_t)j * (Nz + 1) + k] = gy[(size_t)j * (nz + 1) + z0 + k];
+                    z[(size_t)j * (Nz + 1) + k] = gz[(size_t)j * (nz + 1) + z0 + k];
+                }
+        }
         fill_field(u, 0);
         fill_field(v, 1);
         fill_field(w, 2);
@@ -319,7 +329,8 @@ class DIGITAL_FILTER {
         for (int j = 0; j < Ny; ++j)
             for (int k = 0; k < Nz; ++k) {
                 const int idx = j * Nz + k;
-                file << zv_[k] << ", " << yv_[j] << ", " << u.rms[idx] << ", " << v.rms[idx] << ", " << w.rms[idx]
+                const int iidx = j * (Nz + 1) + k; // df.cpp:634-636
+                file << z[iidx] << ", " << y[iidx] << ", " << u.rms[idx] << ", " << v.rms[idx] << ", " << w.rms[idx]
                      << ", " << T_rms[idx] << ", " << rho_rms[idx] << std::endl;
             }
         file.close();
@@ -334,9 +345,9 @@ class DIGITAL_FILTER {
         file << "ZONE T=\"Flow Field\", I=" << Nz + 1 << ", J=" << Ny + 1 << ", F=BLOCK\n";
         file << "VARLOCATION=([3-5]=CELLCENTERED)\n";
         for (int j = 0; j < Ny + 1; ++j)
-            for (int k = 0; k < Nz + 1; ++k) file << zv_[k] << std::endl;
+            for (int k = 0; k < Nz + 1; ++k) file << z[j * (Nz + 1) + k] << std::endl;
         for (int j = 0; j < Ny + 1; ++j)
-            for (int k = 0; k < Nz + 1; ++k) file << yv_[j] << std::endl;
+            for (int k = 0; k < Nz + 1; ++k) file << y[j * (Nz + 1) + k] << std::endl;
         for (const Vector *f : {&u.fluc, &v.fluc, &w.fluc})
             for (int idx = 0; idx < n_cells; ++idx) file << (*f)[idx] << std::endl;
         file.close();
@@ -379,8 +390,9 @@ class DIGITAL_FILTER {
         file << std::setprecision(15) << std::fixed;
         for (int j = 0; j < Ny; ++j)
             for (int k = 0; k < Nz; ++k) {
-                const double yc = 0.25 * (yv_[j] + yv_[j] + yv_[j + 1] + yv_[j + 1]);
-                const double zc = 0.25 * (zv_[k] + zv_[k + 1] + zv_[k] + zv_[k + 1]);
+                const int n00 = j * (Nz + 1) + k, n01 = n00 + 1, n10 = n00 + Nz + 1, n11 = n10 + 1; // df.cpp:775-785
+                const double yc = 0.25 * (y[n00] + y[n01] + y[n10] + y[n11]);
+                const double zc = 0.25 * (z[n00] + z[n01] + z[n10] + z[n11]);
                 const int c = j * Nz + k;
                 file << zc << "," << yc << "," << u.fluc[c] << "," << v.fluc[c] << "," << w.fluc[c] << ","
                      << T_fluc[c] << "," << rho_fluc[c] << "\n";

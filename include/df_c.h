@@ -34,7 +34,11 @@ enum df_status {
     DF_ECOMM = -6     /* RCCL failure (multi-GPU z-strips)                    */
 };
 
-enum df_plane { DF_PLANE_NATIVE = 0, DF_PLANE_SYNTHETIC = 1 };
+enum df_plane {
+    DF_PLANE_NATIVE = 0,    /* read_grid()'s built-in 560 x 400 grid (df.cpp:71-118) */
+    DF_PLANE_SYNTHETIC = 1, /* SURVEY 8d benchmark planes (Ny, Nz, N_min, N_max) */
+    DF_PLANE_GRID = 2       /* a real inflow grid: grid_y/grid_z vertices or grid_file */
+};
 enum df_coeff_mode {
     DF_COEFF_PACKED = 0, /* stream the per-cell coefficient vectors by/bz from HBM (reference data contract) */
     DF_COEFF_TABLE = 1   /* read b(N,i) from a per-N table: same values, no B stream */
@@ -55,7 +59,8 @@ enum df_row {
 typedef struct df_config_c {
     double d_i, rho_e, U_e, mu_e;          /* df.hpp:39-42 */
     int vel_file_offset, vel_file_N_values; /* df.hpp:44-45 (unused by the reference too) */
-    const char *grid_file;                 /* df.hpp:47 (reference has no grid reader; ignored) */
+    const char *grid_file;                 /* df.hpp:47: DF_PLANE_GRID without grid_y/grid_z reads this
+                                              Tecplot BLOCK file (write_tecplot's layout, df.cpp:712-762) */
     const char *vel_fluc_file;             /* df.hpp:48: RST profile (reference reads ../files/RST.dat, df.cpp:224) */
     /* ---- extensions ---- */
     const char *line_file;                 /* mean profile (reference ../line.dat, df.cpp:16) */
@@ -75,6 +80,10 @@ typedef struct df_config_c {
     int rng_saved_flag;                    /*    instead of seeding (checkpoint/resume, and continuing */
     uint64_t rng_state;                    /*    the reference's process-wide stream across instances) */
     double rng_saved;
+    /* DF_PLANE_GRID: (Ny+1)*(Nz+1) vertex coordinates, index j*(Nz+1)+k, row 0 at the wall,
+     * Ny x Nz cells (the Ny/Nz fields above). Per-cell dy, dz, yc follow df.cpp:104-116 with
+     * dz = z[j,k+1] - z[j,k]; half-widths are then per cell (df.cpp:144-195). Copied at create. */
+    const double *grid_y, *grid_z;
 } df_config_c;
 
 typedef struct df_handle df_handle;
@@ -153,6 +162,12 @@ long long df_rms_count(df_handle *h);
 /* Grid vertices used by the reference's writers: y per vertex row (Ny+1) and
  * z per vertex column (Nz+1, global); y/z do not vary along the other axis. */
 int df_get_vertices(df_handle *h, double *y, double *z);
+/* All grid vertices (the reference's y and z vectors, df.hpp:61): (Ny+1)*(Nz+1) each,
+ * index j*(Nz+1)+k, global Nz. Exact on every plane kind (on a grid plane y and z vary
+ * along both axes; df_get_vertices then returns column 0 of y and row 0 of z). */
+int df_get_grid(df_handle *h, double *y, double *z);
+/* Plane kind (enum df_plane) and whether any half-width varies along a row. */
+int df_plane_info(df_handle *h, int *plane, int *per_cell);
 
 /* Device-side coupling handoff (the CFD inflow hook us3d_user.f90:51-130
  * sets ghost-cell u = U + u'): for i < n, on the handle's stream after df_filter,

@@ -27,7 +27,7 @@ module df_c_binding
     integer(c_int), parameter :: DF_OK = 0
     integer(c_int), parameter :: DF_U = 0, DF_V = 1, DF_W = 2, DF_T = 3, DF_RHO = 4
     integer(c_int), parameter :: DF_FILT_OLD_U = 5, DF_FILT_OLD_V = 6, DF_FILT_OLD_W = 7
-    integer(c_int), parameter :: DF_PLANE_NATIVE = 0, DF_PLANE_SYNTHETIC = 1
+    integer(c_int), parameter :: DF_PLANE_NATIVE = 0, DF_PLANE_SYNTHETIC = 1, DF_PLANE_GRID = 2
     integer(c_int), parameter :: DF_COEFF_PACKED = 0, DF_COEFF_TABLE = 1
     integer(c_int), parameter :: DF_ROW_R11 = 0, DF_ROW_R21 = 1, DF_ROW_R22 = 2, DF_ROW_R33 = 3, &
                                  DF_ROW_US = 4, DF_ROW_TS = 5, DF_ROW_RHOS = 6, DF_ROW_MS = 7, &
@@ -46,6 +46,7 @@ module df_c_binding
         integer(c_int) :: rows_per_wave, rng_resume, rng_saved_flag
         integer(c_int64_t) :: rng_state
         real(c_double) :: rng_saved
+        type(c_ptr) :: grid_y, grid_z
     end type df_config_c
 
     interface
@@ -187,7 +188,8 @@ module DIGITAL_FILTERING
     private
     public :: digital_filter_type, create_digital_filter, filter, destroy_digital_filter, DFConfig, FilterField
     public :: get_rms, rng_state, device_fluc, gather_fluc
-    public :: DF_U, DF_V, DF_W, DF_T, DF_RHO, DF_PLANE_NATIVE, DF_PLANE_SYNTHETIC, DF_COEFF_PACKED, DF_COEFF_TABLE
+    public :: DF_U, DF_V, DF_W, DF_T, DF_RHO, DF_PLANE_NATIVE, DF_PLANE_SYNTHETIC, DF_PLANE_GRID
+    public :: DF_COEFF_PACKED, DF_COEFF_TABLE
 
     integer, parameter :: dp = selected_real_kind(15)
 
@@ -199,8 +201,11 @@ module DIGITAL_FILTERING
         character(len=256) :: grid_file = '', vel_fluc_file = ''
         character(len=256) :: line_file = ''
         integer(c_int64_t) :: seed = -1_c_int64_t   ! < 0: seed from random_device like the reference
-        integer :: plane = 0                         ! DF_PLANE_NATIVE / DF_PLANE_SYNTHETIC
+        integer :: plane = 0                         ! DF_PLANE_NATIVE / DF_PLANE_SYNTHETIC / DF_PLANE_GRID
         integer :: Ny = 0, Nz = 0, N_min = 0, N_max = 0
+        ! DF_PLANE_GRID: the inflow grid's vertices, (Ny+1)*(Nz+1) each, index j*(Nz+1)+k+1
+        ! (Ny x Nz cells, row 1 at the wall); unallocated -> grid_file (Tecplot BLOCK, write_tecplot layout)
+        real(kind=dp), allocatable :: grid_y(:), grid_z(:)
         integer :: coeff_mode = 0                    ! DF_COEFF_PACKED / DF_COEFF_TABLE
         character(len=256) :: csv_file = ''          ! non-blank: reference CSV after every filter
         integer :: device = 0                        ! HIP device; -1 = host-only handle (setup queries)
@@ -282,6 +287,7 @@ contains
         type(digital_filter_type) :: DF
         type(df_config_c) :: c
         character(kind=c_char), allocatable, target :: s_grid(:), s_rst(:), s_line(:), s_csv(:)
+        real(c_double), allocatable, target :: gy(:), gz(:)
         integer(c_int) :: Ny, Nz, z0, z1
         integer :: comp
 
@@ -311,6 +317,12 @@ contains
         c%N_max = config%N_max
         c%coeff_mode = config%coeff_mode
         c%device = config%device
+        if (allocated(config%grid_y) .and. allocated(config%grid_z)) then
+            gy = config%grid_y
+            gz = config%grid_z
+            c%grid_y = c_loc(gy)
+            c%grid_z = c_loc(gz)
+        end if
         if (config%rng_resume) then
             c%rng_resume = 1
             c%rng_state = config%rng_state

@@ -305,3 +305,65 @@ def test_set_rng_state_discards_prefetched_noise():
     y.filter(1e-8)
     for k in FIELDS:
         assert np.array_equal(x.field(k), y.field(k))
+
+
+# ---------------------------------------------------------------- grid planes
+
+def _grid_case(name="grid_s3"):
+    return np.load(os.path.join(GOLDEN, name + ".npz"))
+
+
+@pytest.mark.parametrize("mode,rpw", [("packed", 0), ("packed", 1), ("packed", 8), ("table", 0), ("table", 2)])
+def test_golden_grid_plane_per_cell_halfwidths(mode, rpw):
+    """Per-cell N (the reference's calculate_filter_properties on a real grid) vs the
+    reference's own fields (tests/golden/grid_s3, gen_golden.grid_fixture)."""
+    g = _grid_case()
+    st = (int(g["start_state"]), int(g["start_saved_flag"]), float(g["start_saved"]))
+    f = dfamd.DigitalFilter(plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"], device=0, resume=st,
+                            coeff_mode=mode, rows_per_wave=rpw)
+    assert f.plane_info() == (2, True)
+    o = O.Filter(plane=O.PLANE_GRID, Ny=int(g["Ny_in"]), Nz=int(g["Nz_in"]), grid_y=g["grid_y"],
+                 grid_z=g["grid_z"], rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))
+    assert f.rng_state() == o.rng.state
+    full = set(int(x) for x in g["full_steps"])
+    for s in range(int(g["nsteps"]) + 1):
+        if s:
+            f.filter(float(g["dt"]))
+            o.filter(float(g["dt"]))
+            assert f.rng_state() == o.rng.state
+        for k in FIELDS:
+            a = f.field(k)
+            st3 = np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
+            assert np.allclose(st3, g[f"s{s}_{k}_stats"], rtol=1e-9, atol=1e-300), (s, k)
+            if s in full:
+                assert float(rel_err(a, g[f"s{s}_{k}"]).max()) <= TOL, (s, k)
+
+
+@pytest.mark.parametrize("mode", ["packed", "table"])
+def test_grid_plane_vs_oracle_three_strips(mode):
+    # another grid: 3 column strips (Nz = 300), steeper spacing, other phase and seed
+    gy, gz = O.warped_grid(40, 300, dz0=3.0e-5, wave=0.2, seed_phase=1.0)
+    f = dfamd.DigitalFilter(plane="grid", grid_y=gy, grid_z=gz, device=0, seed=17, coeff_mode=mode)
+    o = O.Filter(plane=O.PLANE_GRID, Ny=40, Nz=300, grid_y=gy, grid_z=gz, seed=17)
+    assert f.plane_info()[1]
+    for dt in (None, 1e-8, 2e-8):
+        if dt is not None:
+            f.filter(dt)
+            o.filter(dt)
+        assert f.rng_state() == o.rng.state
+        for k in FIELDS:
+            assert float(rel_err(f.field(k), o.field(k)).max()) <= TOL, (dt, k)
+
+
+def test_grid_plane_table_equals_packed_and_strips_equal_whole():
+    g = _grid_case()
+    kw = dict(plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"], device=0, seed=8)
+    a = dfamd.DigitalFilter(coeff_mode="packed", **kw)
+    b = dfamd.DigitalFilter(coeff_mode="table", **kw)
+    strips = dfamd.create_group(2, **kw)
+    a.filter(1e-8)
+    b.filter(1e-8)
+    dfamd.filter_group(strips, 1e-8)
+    for k in FIELDS:
+        assert np.array_equal(a.field(k), b.field(k)), k
+        assert np.array_equal(np.concatenate([s.field(k) for s in strips], axis=1), a.field(k)), k

@@ -165,3 +165,96 @@ def test_d_i_from_config_changes_the_setup():
     b = dfamd.DigitalFilter(device=-1, seed=1, plane="synthetic", Ny=32, Nz=8, N_min=2, N_max=8, d_i=0.002)
     assert not np.array_equal(a.row("yc"), b.row("yc"))
     assert np.allclose(b.row("yc") / a.row("yc"), 0.002 / 0.0013)
+
+
+# ---------------------------------------------------------------- grid planes
+
+def _grid_golden():
+    return np.load(os.path.join(GOLDEN, "grid_s3.npz"))
+
+
+def test_grid_plane_setup_matches_reference():
+    g = _grid_golden()
+    f = dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"])
+    assert (f.Ny, f.Nz) == (int(g["Ny"]), int(g["Nz"]))  # RST truncation (df.cpp:280-288)
+    assert f.plane_info() == (2, True)
+    for r in ROWS8:
+        assert np.array_equal(f.row(r), g["row_" + r]), r
+    for c, n in enumerate("uvw"):  # per-cell half-widths of the reference's calculate_filter_properties
+        assert np.array_equal(f.halfwidths(c, "y"), g["Ny_" + n]), n
+        assert np.array_equal(f.halfwidths(c, "z"), g["Nz_" + n]), n
+    o = O.Filter(plane=O.PLANE_GRID, Ny=int(g["Ny_in"]), Nz=int(g["Nz_in"]), grid_y=g["grid_y"],
+                 grid_z=g["grid_z"], seed=1)
+    n = o.Ny * o.Nz
+    for c in range(3):
+        F = o.comp(c)
+        assert np.array_equal(f.coeffs(c, "y"), np.ctypeslib.as_array(F.by, shape=(F.by_size,)))
+        assert np.array_equal(f.coeffs(c, "z"), np.ctypeslib.as_array(F.bz, shape=(F.bz_size,)))
+        assert np.array_equal(f.offsets(c, "y").ravel(), np.ctypeslib.as_array(F.by_offsets, shape=(n,)))
+        assert np.array_equal(f.offsets(c, "z").ravel(), np.ctypeslib.as_array(F.bz_offsets, shape=(n,)))
+    assert f.stream_length() == sum(O.stream_lengths(o))
+    y, z = f.grid()
+    assert np.array_equal(y, g["grid_y"][: f.Ny + 1]) and np.array_equal(z, g["grid_z"][: f.Ny + 1])
+
+
+def _write_tecplot_grid(path, gy, gz, y_first=False):
+    J, I = gy.shape
+    with open(path, "w") as fh:
+        names = '"y", "z"' if y_first else '"z", "y"'
+        fh.write(f"VARIABLES = {names}, \"u_fluc\", \"v_fluc\", \"w_fluc\" \n")
+        fh.write(f'ZONE T="Flow Field", I={I}, J={J}, F=BLOCK\n')
+        fh.write("VARLOCATION=([3-5]=CELLCENTERED)\n")
+        for a in ((gy, gz) if y_first else (gz, gy)):
+            fh.write("\n".join(repr(float(v)) for v in a.ravel()) + "\n")
+
+
+@pytest.mark.parametrize("y_first", [False, True])
+def test_grid_plane_from_tecplot_file(tmp_path, y_first):
+    # grid_file (df.hpp:47) in write_tecplot's BLOCK layout (df.cpp:712-762)
+    g = _grid_golden()
+    p = tmp_path / "grid.dat"
+    _write_tecplot_grid(p, g["grid_y"], g["grid_z"], y_first)
+    f = dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_file=str(p))
+    a = dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"])
+    assert (f.Ny, f.Nz) == (a.Ny, a.Nz)
+    for c in range(3):
+        for d in "yz":
+            assert np.array_equal(f.halfwidths(c, d), a.halfwidths(c, d))
+
+
+def test_row_uniform_grid_is_not_per_cell():
+    # the reference's own placeholder grid fed back as vertices: per-row N, identical setup
+    nat = host()
+    y, z = nat.grid()
+    f = dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_y=y, grid_z=z)
+    assert f.plane_info() == (2, False)
+    for c in range(3):
+        for d in "yz":
+            assert np.array_equal(f.halfwidths(c, d), nat.halfwidths(c, d))
+
+
+def test_grid_plane_rejects_bad_vertices(tmp_path):
+    g = _grid_golden()
+    bad = g["grid_z"].copy()
+    bad[:, 5] = bad[:, 4]  # zero-width column
+    with pytest.raises(dfamd.DFError, match="increase"):
+        dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_y=g["grid_y"], grid_z=bad)
+    with pytest.raises(dfamd.DFError, match="grid plane needs"):
+        dfamd.DigitalFilter(device=-1, seed=1, plane="grid", Ny=4, Nz=4)
+    p = tmp_path / "g.dat"
+    p.write_text("VARIABLES = \"z\", \"y\"\nZONE I=3, J=3\n1 2 3\n")
+    with pytest.raises(dfamd.DFError, match="fewer values"):
+        dfamd.DigitalFilter(device=-1, seed=1, plane="grid", grid_file=str(p))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_grid_plane_strips_partition_coefficients(world):
+    g = _grid_golden()
+    kw = dict(device=-1, seed=1, plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"])
+    whole = dfamd.DigitalFilter(**kw)
+    strips = [dfamd.DigitalFilter(rank=r, world=world, **kw) for r in range(world)]
+    for c in range(3):
+        for d in "yz":
+            assert np.array_equal(np.concatenate([s.halfwidths(c, d) for s in strips], axis=1),
+                                  whole.halfwidths(c, d))
+        assert sum(s.comp_info(c)["by_size"] for s in strips) == whole.comp_info(c)["by_size"]

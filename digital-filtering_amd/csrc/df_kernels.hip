@@ -19,10 +19,22 @@ namespace dfamd {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Timing-only ablations (Makefile `variant`): DF_ABLATE_NOISE replaces every noise load
+// of the sweeps by a register value, DF_ABLATE_COEF every coefficient load. Results are
+// wrong by design; the product is never built with either.
+#if defined(DF_ABLATE_NOISE)
+#define DF_NOISE(ptr, tag) make_double2((double)(tag), (double)(threadIdx.x & 63))
+#else
+#define DF_NOISE(ptr, tag) (*(ptr))
+#endif
+
 // Coefficient stream load: read once per call, so optionally non-temporal.
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
 {
+#if defined(DF_ABLATE_COEF)
+    return make_double2((double)(size_t)p, 1.0);
+#endif
     if (NT) {
         const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(p));
         return make_double2(v.x, v.y);
@@ -487,7 +499,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
     };
     auto predicated = [&](int t) {
-        const double2 n = *reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz);
+        const double2 n = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int i = t - r;
@@ -499,7 +511,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         }
     };
     auto body = [&](int t) {
-        const double2 n = *reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz);
+        const double2 n = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t);
         double2 b[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) b[r] = coef(r, t);
@@ -617,11 +629,11 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
         };
         double acc0 = 0.0, acc1 = 0.0;
-        double2 P = xp[0];
+        double2 P = DF_NOISE(xp, 0);
         int m = 0;
         if (ZU >= 4) {
             for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
-                const double2 P1 = xp[m + 1], P2 = xp[m + 2], P3 = xp[m + 3], P4 = xp[m + 4];
+                const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2), P3 = DF_NOISE(xp + m + 3, m + 3), P4 = DF_NOISE(xp + m + 4, m + 4);
                 double2 b[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) b[u] = coef(2 * m + u);
@@ -645,7 +657,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             }
         }
         for (; m + 2 <= N; m += 2) {
-            const double2 P1 = xp[m + 1], P2 = xp[m + 2];
+            const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2);
             const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
             acc0 += b0.x * P.x;
             acc1 += b0.y * P.y;
@@ -658,7 +670,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             P = P2;
         }
         for (; m < N; ++m) {
-            const double2 P1 = xp[m + 1];
+            const double2 P1 = DF_NOISE(xp + m + 1, m + 1);
             const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1);
             acc0 += b0.x * P.x;
             acc1 += b0.y * P.y;

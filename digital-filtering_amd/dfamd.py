@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdfamd.so")
+# DFAMD_LIB: a timing-only kernel variant (Makefile `variant` target, tools/variant_ab.sh)
+LIB_PATH = os.environ.get("DFAMD_LIB") or os.path.join(HERE, "libdfamd.so")
 DATA = os.path.join(HERE, "data")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "df_c.h")
 

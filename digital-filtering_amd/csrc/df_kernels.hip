@@ -352,27 +352,56 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         const int n_acc = __popcll(mask);
         const uint64_t q_first = f + 2ull * (uint64_t)rank0;
         const uint64_t q_end = q_first + 2ull * (uint64_t)n_acc; // exclusive
-        const StreamPos P0 = stream_pos(T, q_first);
-        const bool fast = n_acc > 0 && T.width[P0.sidx] >= 2 * 64 && q_end <= T.seg[P0.sidx + 1];
+        // Wave-level position from the kernel-argument tables: q_first is uniform, so this
+        // runs on the SALU with scalar loads (the LDS copy T serves per-lane lookups only).
+        const StreamPos P0 = stream_pos(g, q_first);
+        const int su = uniform(P0.sidx);
+        const bool fast = n_acc > 0 && g.width[su] >= 2 * 64 && q_end <= g.seg[su + 1];
+        // Wave-uniform skip (SALU): the run [q_first, q_end) stays in one row of one array and
+        // every column it covers is one this GPU never stores (the r_zs interior, df.cpp:377,
+        // or another strip's r_ys columns), and it does not hold the call's last attempt.
+        bool idle = n_acc == 0;
+        if (fast && !(rank0 <= A - 1 && A - 1 < rank0 + n_acc)) {
+            const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n_acc, W = g.width[su];
+            if (c1 <= W) {
+                if (su & 1) {
+                    const uint32_t nzp = (uint32_t)g.Nzp[su >> 1];
+                    idle = (!g.is_first || c0 >= nzp) && (!g.is_last || c1 <= nzp + (uint32_t)g.Nz_g);
+                } else {
+                    idle = c1 <= (uint32_t)g.z0 || c0 >= (uint32_t)g.z1;
+                }
+            }
+        }
+        if (idle) {
+            st = g.next_mult * st + g.next_plus;
+            continue;
+        }
         if (acc) {
             const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
             const long long rank = rank0 + below;
             if (rank < A) {
                 const uint64_t q0 = q_first + 2ull * (uint64_t)below;
-                StreamPos p0;
-                if (fast) {
-                    p0 = P0;
-                    p0.col += 2u * (uint32_t)below;
-                    if (p0.col >= T.width[P0.sidx]) {
-                        p0.col -= T.width[P0.sidx];
+                double *d0, *d1;
+                if (fast) { // one array, at most one row wrap: uniform array index, scalar tables
+                    const uint32_t W = g.width[su];
+                    StreamPos p0 = {su, P0.row, P0.col + 2u * (uint32_t)below};
+                    if (p0.col >= W) {
+                        p0.col -= W;
                         p0.row++;
                     }
+                    StreamPos p1 = {su, p0.row, p0.col + 1u}; // q0 + 1 < q_end <= end of array su
+                    if (p1.col == W) {
+                        p1.col = 0;
+                        p1.row++;
+                    }
+                    d0 = stream_dest(g, p0);
+                    d1 = stream_dest(g, p1);
                 } else {
-                    p0 = stream_pos(T, q0);
+                    const StreamPos p0 = stream_pos(T, q0);
+                    d0 = stream_dest(T, p0);
+                    d1 = (q0 + 1 < g.Q) ? stream_dest(T, stream_next(T, p0)) : nullptr;
                 }
-                double *d0 = stream_dest(T, p0);
-                double *d1 = (q0 + 1 < g.Q) ? stream_dest(T, stream_next(T, p0)) : nullptr;
                 const bool last = (rank == A - 1);
                 if (d0 || d1 || last) {
                     uint64_t s4 = st;

@@ -96,6 +96,7 @@ struct df_handle {
     RngStateDev *rstate = nullptr; // [2], ping-pong by call parity
     int *counts = nullptr;
     long long *offsets = nullptr;
+    long long *part = nullptr; // K2a run totals -> run prefixes (K2b)
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
     int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped
     int *err_host = nullptr;
@@ -266,9 +267,11 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
     const int set = (int)(h->gen_launched & 1);
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
+    // every rank holds every block's accept masks (gathered with the counts), so K3 never
+    // redraws accept decisions
     HIP_OR(launch_rng_finish(g, h->rstate + (h->gen_launched & 1), h->rstate + ((h->gen_launched + 1) & 1),
-                             h->counts, h->offsets, h->masks, h->err_dev, h->rng_blocks, nb_scan,
-                             h->split_count ? h->own_b0 : 0, h->split_count ? h->own_b1 : h->rng_blocks, rs),
+                             h->counts, h->offsets, h->part, h->masks, h->err_dev, h->rng_blocks, nb_scan, 0,
+                             h->rng_blocks, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5);
     HIP_OR(hipEventRecord(h->ev_rng[set], rs), DF_EHIP);
@@ -299,6 +302,9 @@ int launch_gen_group(std::vector<df_handle *> &hs)
             HIP_OR(hipMemcpyAsync(h->counts + at, hs[o]->counts + at, h->rng_chunk * sizeof(int), hipMemcpyDefault,
                                   rss[r]),
                    DF_EHIP);
+            HIP_OR(hipMemcpyAsync(h->masks + at * kRngThreads, hs[o]->masks + at * kRngThreads,
+                                  (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t), hipMemcpyDefault, rss[r]),
+                   DF_EHIP);
         }
         if ((rc = gen_end(h, gs[r], rss[r]))) return rc;
     }
@@ -318,14 +324,23 @@ int launch_gen(df_handle *h)
     if (rc) return rc;
     if (h->split_count) {
         int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
-        if (h->rng_comm) { // the one collective of the RNG: per-block accept counts
+        const size_t mbytes = (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t);
+        uint16_t *mmine = h->masks + (size_t)h->rank * h->rng_chunk * kRngThreads;
+        if (h->rng_comm) { // the RNG's one exchange: per-block accept counts and masks
+            NCCL_OR(ncclGroupStart());
             NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
-        } else { // DFAMD_SOLO_STRIP timing mode: stand-in counts for the other ranks' shares
+            NCCL_OR(ncclAllGather(mmine, h->masks, mbytes, ncclUint8, h->rng_comm, rs));
+            NCCL_OR(ncclGroupEnd());
+        } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
             for (int o = 0; o < h->world; ++o)
-                if (o != h->rank)
+                if (o != h->rank) {
                     HIP_OR(hipMemcpyAsync(h->counts + (size_t)o * h->rng_chunk, mine, h->rng_chunk * sizeof(int),
                                           hipMemcpyDeviceToDevice, rs),
                            DF_EHIP);
+                    HIP_OR(hipMemcpyAsync(h->masks + (size_t)o * h->rng_chunk * kRngThreads, mmine, mbytes,
+                                          hipMemcpyDeviceToDevice, rs),
+                           DF_EHIP);
+                }
         }
     }
     return gen_end(h, g, rs);
@@ -539,10 +554,10 @@ int build(df_handle *h, const df_config_c *cfg)
         // ceil(2^64 / W): floor(p * inv / 2^64) == p / W for every p < 2^32
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
-    const PcgJump hop = pcg_jump(4ull * (kRngThreads - 1));
+    const PcgJump hop = pcg_jump(4ull * (64 - 1)); // after an attempt's 4 draws -> the lane's next attempt
     g.hop_mult = hop.mult;
     g.hop_plus = hop.plus;
-    const PcgJump next = pcg_jump(4ull * kRngThreads); // attempt start -> the thread's next attempt start
+    const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
     g.next_mult = next.mult;
     g.next_plus = next.plus;
     g.Nz_g = s.Nz;
@@ -698,19 +713,24 @@ int build(df_handle *h, const df_config_c *cfg)
     h->own_b1 = std::min(h->own_b0 + h->rng_chunk, h->rng_blocks);
     if ((rc = dalloc_t(h, &h->counts, nb_pad))) return rc;
     if ((rc = dalloc_t(h, &h->offsets, nb_pad))) return rc;
+    if ((nb_pad + 1023) / 1024 > 1024) return fail(DF_EINVAL, "plane too large for the RNG scan (> 2^20 attempt blocks)");
+    if ((rc = dalloc_t(h, &h->part, (nb_pad + 1023) / 1024))) return rc;
     if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
     HIP_OR(hipEventCreateWithFlags(&h->ev_counted, hipEventDisableTiming), DF_EHIP);
     {
-        // jump tables: block b starts 4*4096*b outputs in, thread tid 4*tid further
+        // jump tables: block b starts 4*4096*b outputs in; thread tid = 64*w + l starts
+        // 4*(1024*w + l) further (wave w owns attempts [1024*w, 1024*(w+1)) of the block)
         auto compose = [](PcgJumpDev a, PcgJump b) { // b after a
             return PcgJumpDev{b.mult * a.mult, b.mult * a.plus + b.plus};
         };
         std::vector<PcgJumpDev> jb(nb_pad), jt(kRngThreads);
-        const PcgJump blk = pcg_jump(4ull * kRngBlockAttempts), one = pcg_jump(4);
+        const PcgJump blk = pcg_jump(4ull * kRngBlockAttempts);
         jb[0] = PcgJumpDev{1, 0};
         for (int b = 1; b < nb_pad; ++b) jb[b] = compose(jb[b - 1], blk);
-        jt[0] = PcgJumpDev{1, 0};
-        for (int t = 1; t < kRngThreads; ++t) jt[t] = compose(jt[t - 1], one);
+        for (int t = 0; t < kRngThreads; ++t) {
+            const PcgJump j = pcg_jump(4ull * (uint64_t)((t >> 6) * (kRngBlockAttempts / 4) + (t & 63)));
+            jt[t] = PcgJumpDev{j.mult, j.plus};
+        }
         PcgJumpDev *djb = nullptr, *djt = nullptr;
         if ((rc = dalloc_t(h, &djb, jb.size()))) return rc;
         if ((rc = dalloc_t(h, &djt, jt.size()))) return rc;

@@ -85,11 +85,13 @@ hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st
 //
 // Attempt t (0-based within the call) consumes pcg32 outputs 4t..4t+3 of the
 // stream that starts at the call's state S. Block b owns attempts
-// [b*4096, (b+1)*4096); thread `tid` handles b*4096 + m*256 + tid, m = 0..15,
-// so consecutive lanes hold consecutive attempts and a wave's accepted attempts
-// map to consecutive stream positions (coalesced stores).
+// [b*4096, (b+1)*4096); wave w of the block owns the contiguous run
+// b*4096 + w*1024 + [0, 1024) and lane l handles b*4096 + w*1024 + m*64 + l,
+// m = 0..15. Consecutive lanes hold consecutive attempts, so a wave's accepted
+// attempts map to consecutive stream positions (coalesced stores), and a wave's
+// whole run covers one contiguous stream range it can test once (K3).
 
-// State at the thread's first attempt, advance(S, 4*(b*4096 + tid)), as two
+// State at the thread's first attempt, advance(S, 4*(b*4096 + w*1024 + l)), as two
 // affine steps from host-built jump tables (pcg_random.hpp:639-662 composed).
 __device__ __forceinline__ uint64_t thread_first_state(const RngGeom &g, uint64_t S, int b, int tid)
 {
@@ -131,34 +133,59 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
     }
 }
 
-__global__ __launch_bounds__(1024) void rng_scan_kernel(const int *__restrict__ counts,
-                                                       long long *__restrict__ offsets, int nblocks,
-                                                       const RngStateDev *__restrict__ sin, uint64_t Q,
-                                                       int *__restrict__ err)
+// K2: exclusive scan of the per-block accept counts in two levels, so no thread walks a long
+// serial run (a single-block scan took 58 us for the 33k blocks of an 8-GPU plane):
+// K2a scans each run of 1024 counts (4 per thread, wave shuffles + one LDS pass) into
+// offsets[] and writes the run's total to part[]; K2b scans part[] in one block. A block's
+// global offset is offsets[b] + part[b >> 10] (read by K3).
+__global__ __launch_bounds__(256) void rng_scan_local_kernel(const int *__restrict__ counts,
+                                                             long long *__restrict__ offsets,
+                                                             long long *__restrict__ part, int nblocks)
 {
-    __shared__ long long part[1024];
+    __shared__ long long wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b0 = blockIdx.x * 1024 + tid * 4;
+    int v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = b0 + i < nblocks ? counts[b0 + i] : 0;
+    const long long t = (long long)v[0] + v[1] + v[2] + v[3];
+    long long x = t; // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    long long excl = x - t;
+    for (int ww = 0; ww < w; ++ww) excl += wsum[ww];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (b0 + i < nblocks) offsets[b0 + i] = excl;
+        excl += v[i];
+    }
+    if (tid == 255) part[blockIdx.x] = excl; // run total
+}
+
+__global__ __launch_bounds__(1024) void rng_scan_parts_kernel(long long *__restrict__ part, int nparts,
+                                                              const RngStateDev *__restrict__ sin, uint64_t Q,
+                                                              int *__restrict__ err)
+{
+    __shared__ long long p[1024];
     const int tid = threadIdx.x;
-    const int chunk = (nblocks + 1023) / 1024;
-    const int b0 = min(tid * chunk, nblocks), b1 = min(b0 + chunk, nblocks);
-    long long s = 0;
-    for (int b = b0; b < b1; ++b) s += counts[b];
-    part[tid] = s;
+    p[tid] = tid < nparts ? part[tid] : 0;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
-        long long v = tid >= o ? part[tid - o] : 0;
+        const long long v = tid >= o ? p[tid - o] : 0;
         __syncthreads();
-        part[tid] += v;
+        p[tid] += v;
         __syncthreads();
     }
-    long long base = tid ? part[tid - 1] : 0;
-    for (int b = b0; b < b1; ++b) {
-        offsets[b] = base;
-        base += counts[b];
-    }
+    if (tid < nparts) part[tid] = tid ? p[tid - 1] : 0;
     if (tid == 1023) {
         const uint64_t f = (uint64_t)sin->saved_flag;
         const long long A = (long long)((Q - f + 1) / 2);
-        if (part[1023] < A) *err = 1; // not enough attempts launched: host re-sizes
+        if (p[1023] < A) *err = 1; // not enough attempts launched: host re-sizes
     }
 }
 
@@ -263,6 +290,7 @@ template <class G> __device__ bool range_needed(const G &g, uint64_t q0, uint64_
 __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                   RngStateDev *__restrict__ sout,
                                                                   const long long *__restrict__ offsets,
+                                                                  const long long *__restrict__ part,
                                                                   const uint16_t *__restrict__ masks,
                                                                   const int *__restrict__ counts, int own_b0,
                                                                   int own_b1)
@@ -273,7 +301,10 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
-    const long long Ob = offsets[blockIdx.x];
+    const long long Ob = offsets[blockIdx.x] + part[blockIdx.x >> 10];
+    const bool own = (int)blockIdx.x >= own_b0 && (int)blockIdx.x < own_b1;
+    // issued early: its latency overlaps the block-level tests below
+    const uint32_t own_bits = own ? masks[(size_t)blockIdx.x * kRngThreads + tid] : 0u;
     if (Ob >= A) return; // uniform: the whole block is past the call's last attempt
     {
         // Blocks whose normals all land on other GPUs' columns (or in the r_zs
@@ -285,19 +316,21 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         const bool holds_last = Oe >= A;
         if (!holds_last && !(blockIdx.x == 0 && f) && !range_needed(g, q_lo, q_hi)) return;
     }
-    if (tid == 0) {
-        for (int i = 0; i < 7; ++i) T.seg[i] = g.seg[i];
-        for (int i = 0; i < 6; ++i) {
-            T.inv_width[i] = g.inv_width[i];
-            T.width[i] = g.width[i];
-            T.rows[i] = g.rows[i];
-        }
-        for (int c = 0; c < 3; ++c) {
-            T.ry[c] = g.ry[c];
-            T.rz[c] = g.rz[c];
-            T.Nzp[c] = g.Nzp[c];
-            T.rz_pitch[c] = g.rz_pitch[c];
-        }
+    if (tid < 7) T.seg[tid] = g.seg[tid];
+    if (tid >= 64 && tid < 70) {
+        const int i = tid - 64;
+        T.inv_width[i] = g.inv_width[i];
+        T.width[i] = g.width[i];
+        T.rows[i] = g.rows[i];
+    }
+    if (tid >= 128 && tid < 131) {
+        const int c = tid - 128;
+        T.ry[c] = g.ry[c];
+        T.rz[c] = g.rz[c];
+        T.Nzp[c] = g.Nzp[c];
+        T.rz_pitch[c] = g.rz_pitch[c];
+    }
+    if (tid == 192) {
         T.Nz_g = g.Nz_g;
         T.Pz = g.Pz;
         T.z0 = g.z0;
@@ -312,9 +345,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         if (d) *d = sin->saved * 1.0 + 0.0;
     }
     uint32_t bits;
-    if ((int)blockIdx.x >= own_b0 && (int)blockIdx.x < own_b1) {
-        bits = masks[(size_t)blockIdx.x * kRngThreads + tid]; // this rank counted the block (K1)
-    } else { // another z-strip rank counted it: redo its accept tests
+    if (own) {
+        bits = own_bits; // K1's accept flags (this rank's count, or gathered from the others)
+    } else { // accept flags not available here: redo the tests
         bits = 0;
         uint64_t sc = thread_first_state(g, sin->state, blockIdx.x, tid);
         for (int m = 0; m < kRngPerThread; ++m) {
@@ -328,15 +361,31 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         if (lane == 0) cnt[m][w] = __popcll(mask);
     }
     __syncthreads();
-    if (tid == 0) {
-        int run = 0;
-        for (int m = 0; m < kRngPerThread; ++m)
-            for (int ww = 0; ww < kRngThreads / 64; ++ww) {
-                pre[m][ww] = run;
-                run += cnt[m][ww];
-            }
+    static_assert(kRngPerThread * (kRngThreads / 64) == 64, "one wave scans the block's (wave, m) counts");
+    if (w == 0) { // ranks in attempt order, wave-major (each wave owns a contiguous run): entry
+                  // e = 16*wave + m, one lane each, exclusive scan by shuffles
+        const int m = lane % kRngPerThread, ww = lane / kRngPerThread;
+        const int v = cnt[m][ww];
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        pre[m][ww] = x - v;
     }
     __syncthreads();
+    {
+        // The wave's accepted attempts own stream positions [f + 2*r_lo, f + 2*r_hi): a wave
+        // whose range stores nothing here (other strips' columns, the r_zs interior) and does
+        // not end the call has no pass 2 at all.
+        const long long r_lo = Ob + uniform(pre[0][w]);
+        const long long r_hi = Ob + uniform(pre[kRngPerThread - 1][w] + cnt[kRngPerThread - 1][w]);
+        const uint64_t q_lo = f + 2ull * (uint64_t)r_lo;
+        const uint64_t q_hi = (f + 2ull * (uint64_t)r_hi) < g.Q ? (f + 2ull * (uint64_t)r_hi) : g.Q;
+        const bool ends_call = r_lo <= A - 1 && A - 1 < r_hi;
+        if (r_lo >= A || (!ends_call && (q_lo >= q_hi || !range_needed(g, q_lo, q_hi)))) return;
+    }
     // Pass 2: ranks come from the K1 accept flags, so an attempt's draws are
     // recomputed only when one of its normals is stored (or it ends the call);
     // every other attempt just jumps the state to the thread's next attempt.
@@ -448,12 +497,14 @@ hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *cou
 }
 
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                             long long *offsets, uint16_t *masks, int *err, int nb_total, int nb_scan, int own_b0,
-                             int own_b1, hipStream_t st)
+                             long long *offsets, long long *part, uint16_t *masks, int *err, int nb_total,
+                             int nb_scan, int own_b0, int own_b1, hipStream_t st)
 {
-    hipLaunchKernelGGL(rng_scan_kernel, dim3(1), dim3(1024), 0, st, counts, offsets, nb_scan, st_in, g.Q, err);
+    const int nparts = (nb_scan + 1023) / 1024; // <= 1024: checked at create
+    hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
+    hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err);
     hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, st_out, offsets,
-                       masks, counts, own_b0, own_b1);
+                       part, masks, counts, own_b0, own_b1);
     return hipGetLastError();
 }
 

@@ -24,6 +24,8 @@ constexpr int kStrip = 128;           // cells per strip (one wave, 2 per lane)
 constexpr int kRngThreads = 256;      // threads per RNG block
 constexpr int kRngPerThread = 16;     // polar attempts per thread
 constexpr int kRngBlockAttempts = kRngThreads * kRngPerThread;
+static_assert(kRngThreads == 256 && kRngPerThread * 64 == kRngBlockAttempts / 4,
+              "RNG mapping: 4 waves per block, each owning a contiguous run of 64 * kRngPerThread attempts");
 
 struct RngStateDev {
     uint64_t state;
@@ -39,10 +41,10 @@ struct PcgJumpDev {
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
-    uint64_t hop_mult, hop_plus;   // jump over (kRngThreads-1)*4 outputs (after an attempt's 4 draws)
-    uint64_t next_mult, next_plus; // jump over kRngThreads*4 outputs (attempt start to the next one)
+    uint64_t hop_mult, hop_plus;   // jump over 63*4 outputs (after an attempt's 4 draws to the lane's next)
+    uint64_t next_mult, next_plus; // jump over 64*4 outputs (attempt start to the lane's next one)
     const PcgJumpDev *jump_block;  // [nblocks]: jump over 4*4096*b outputs
-    const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*tid outputs
+    const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*(1024*(tid/64) + tid%64) outputs
     int Nz_g, Pz, z0, z1, is_first, is_last;
     uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
     int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw
@@ -88,8 +90,8 @@ hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *cou
 // K2 + K3 once every block's count is present; blocks outside [own_b0, own_b1)
 // re-derive their accept flags.
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                             long long *offsets, uint16_t *masks, int *err, int nb_total, int nb_scan, int own_b0,
-                             int own_b1, hipStream_t st);
+                             long long *offsets, long long *part, uint16_t *masks, int *err, int nb_total,
+                             int nb_scan, int own_b0, int own_b1, hipStream_t st);
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st);
 hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
 // Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),

@@ -47,7 +47,7 @@ def parse():
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     p.add_argument("--cpu-cols", type=int, default=512,
                    help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
-    p.add_argument("--cpu-calls", type=int, default=10)
+    p.add_argument("--cpu-calls", type=int, default=16)  # ~13 s of reference CPU work (0.8 s per call)
     p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
                    help="also time the other coefficient mode (N=1 only) and report it under alt_modes")

@@ -472,7 +472,8 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
                     } else if (d0 && d1 == d0 + 1 && ((uintptr_t)d0 & 15) == 0) {
                         // adjacent and aligned (the common case): accepted lanes of a
                         // wave then store one contiguous run of 16-B pairs
-                        *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
+                        if (g.nt_stores) __builtin_nontemporal_store(dvec2{n0, n1}, reinterpret_cast<dvec2 *>(d0));
+                        else *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
                     } else {
                         if (d0) *d0 = n0;
                         if (d1) *d1 = n1;
@@ -626,8 +627,18 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < nr) {
+#if defined(DF_STORE_SINK)
+            double *o = a.rz[c] + a.Nzp[c] + col; // timing only: all rows onto row 0
+#else
             double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + col;
-            if (col + 1 < a.Nz_loc) *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
+#endif
+#if defined(DF_ABLATE_STORE)
+            if (acc0[r] != 1234.5) continue; // timing only
+#endif
+            if (col + 1 < a.Nz_loc) {
+                if (a.nt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
+                else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
+            }
             else if (col < a.Nz_loc) o[0] = acc0[r];
         }
     }
@@ -775,34 +786,68 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         }
         return;
     }
+    if (col >= a.Nz_loc) return;
     const double *rc = a.rowc;
     const double sR11 = rc[j], bb = rc[Ny + j], sR22b = rc[2 * Ny + j], sR33 = rc[3 * Ny + j];
     const double t1 = rc[4 * Ny + j], Ts = rc[5 * Ny + j], rh = rc[6 * Ny + j];
+    // The lane's two cells as one 16-B access per field when the row offset keeps them
+    // aligned (every row when Nz_loc is even), else two 8-B accesses.
+#if defined(DF_STORE_SINK)
+    const size_t idx = (size_t)col; // timing only: every row lands on row 0 (stores stay in L2)
+#else
+    const size_t idx = (size_t)j * a.Nz_loc + col;
+#endif
+    const bool has1 = col + 1 < a.Nz_loc, pair = has1 && (idx & 1) == 0;
+    auto ld = [&](const double *p) -> double2 {
+        if (pair) return *reinterpret_cast<const double2 *>(p + idx);
+        return make_double2(p[idx], has1 ? p[idx + 1] : 0.0);
+    };
+    auto st = [&](double *p, double x, double y) {
+#if defined(DF_ABLATE_STORE)
+        if (x != 1234.5) return; // timing only: keep the values live, store nothing
+#endif
+        if (pair) {
+            if (a.nt_stores) __builtin_nontemporal_store(dvec2{x, y}, reinterpret_cast<dvec2 *>(p + idx));
+            else *reinterpret_cast<double2 *>(p + idx) = make_double2(x, y);
+            return;
+        }
+        p[idx] = x;
+        if (has1) p[idx + 1] = y;
+    };
+    double fu[2] = {f0[0], f1[0]}, fv[2] = {f0[1], f1[1]}, fw[2] = {f0[2], f1[2]};
+    if (a.do_corr) { // df.cpp:415
+        const double2 ou = ld(a.filt_old[0]), ov = ld(a.filt_old[1]), ow = ld(a.filt_old[2]);
+        const double o[3][2] = {{ou.x, ou.y}, {ov.x, ov.y}, {ow.x, ow.y}};
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            fu[e] = o[0][e] * a.sa[0] + fu[e] * a.s1a[0];
+            fv[e] = o[1][e] * a.sa[1] + fv[e] * a.s1a[1];
+            fw[e] = o[2][e] * a.sa[2] + fw[e] * a.s1a[2];
+        }
+    }
+    double up[2], vp[2], wp[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-        const int k = col + e;
-        if (k >= a.Nz_loc) continue;
-        const size_t idx = (size_t)j * a.Nz_loc + k;
-        double fu = e ? f1[0] : f0[0], fv = e ? f1[1] : f0[1], fw = e ? f1[2] : f0[2];
-        if (a.do_corr) { // df.cpp:415
-            fu = a.filt_old[0][idx] * a.sa[0] + fu * a.s1a[0];
-            fv = a.filt_old[1][idx] * a.sa[1] + fv * a.s1a[1];
-            fw = a.filt_old[2][idx] * a.sa[2] + fw * a.s1a[2];
+        up[e] = sR11 * fu[e];              // df.cpp:436
+        vp[e] = bb * fu[e] + sR22b * fv[e]; // df.cpp:437
+        wp[e] = sR33 * fw[e];              // df.cpp:438
+    }
+    st(a.fluc[0], up[0], up[1]);
+    st(a.fluc[1], vp[0], vp[1]);
+    st(a.fluc[2], wp[0], wp[1]);
+    st(a.filt_old[0], fu[0], fu[1]); // df.cpp:440-442
+    st(a.filt_old[1], fv[0], fv[1]);
+    st(a.filt_old[2], fw[0], fw[1]);
+    if (a.do_sra) { // df.cpp:474-481
+        double T2[2], R2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const double t2 = t1 * up[e];
+            T2[e] = t2 * Ts;
+            R2[e] = -t2 * rh;
         }
-        const double up = sR11 * fu;             // df.cpp:436
-        const double vp = bb * fu + sR22b * fv;  // df.cpp:437
-        const double wp = sR33 * fw;             // df.cpp:438
-        a.fluc[0][idx] = up;
-        a.fluc[1][idx] = vp;
-        a.fluc[2][idx] = wp;
-        a.filt_old[0][idx] = fu; // df.cpp:440-442
-        a.filt_old[1][idx] = fv;
-        a.filt_old[2][idx] = fw;
-        if (a.do_sra) { // df.cpp:474-481
-            const double t2 = t1 * up;
-            a.T[idx] = t2 * Ts;
-            a.rho[idx] = -t2 * rh;
-        }
+        st(a.T, T2[0], T2[1]);
+        st(a.rho, R2[0], R2[1]);
     }
 }
 

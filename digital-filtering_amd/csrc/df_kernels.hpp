@@ -48,6 +48,7 @@ struct RngGeom {
     int Nz_g, Pz, z0, z1, is_first, is_last;
     uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
     int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw
+    int nt_stores;                 // noise pairs stored non-temporally
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];
@@ -75,7 +76,8 @@ struct SweepArgs {
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
     int nt_loads;           // non-temporal loads for the coefficient stream
     int heavy_first;        // schedule rows with the widest stencils first
-    int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
+    int yunroll, zunroll;
+    int nt_stores;                        // sweep outputs stored non-temporally   // taps per loop iteration (tuning knobs)
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.

@@ -179,7 +179,7 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
                     const long long *dst_cell, long long dst_len, double beta);
 
 /* Launch-shape tuning (extension; results are bit-identical for every setting):
- * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4), "zunroll" (2,4). */
+ * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4), "zunroll" (2,4), "nt_stores", "rng_nt_stores". */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* Timing (hipEvents on the handle's stream). */

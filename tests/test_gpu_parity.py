@@ -207,7 +207,8 @@ def test_runtime_tuning_is_bitexact(mode):
     a = gpu_synth(*spec, seed=5, coeff_mode=mode)
     b = gpu_synth(*spec, seed=5, coeff_mode=mode)
     settings = [dict(rows_per_wave=1, zunroll=4, yunroll=4), dict(rows_per_wave=8, nt_loads=0, heavy_first=0),
-                dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_loads=1, heavy_first=1)]
+                dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_loads=1, heavy_first=1, nt_stores=1),
+                dict(nt_stores=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

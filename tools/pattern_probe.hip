@@ -52,6 +52,34 @@ __global__ __launch_bounds__(256) void chunk_kernel(const dvec2 *__restrict__ p,
     if (acc.x == 123.456 && acc.y == 654.321) *sink = acc.x;
 }
 
+// chunk pattern (G = 0, U = 4) plus Wk 1-KiB writes per wave after its chunk (output runs
+// contiguous in chunk order), to price a small write fraction inside a read stream.
+__global__ __launch_bounds__(256) void chunk_write_kernel(const dvec2 *__restrict__ p, dvec2 *__restrict__ out,
+                                                          int nchunks, int S, int Wk, int nt_store)
+{
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nw = gridDim.x * 4;
+    for (int c = wave; c < nchunks; c += nw) {
+        const dvec2 *q = p + (size_t)c * S * 64 + lane;
+        dvec2 acc = {0, 0};
+        int s = 0;
+        for (; s + 4 <= S; s += 4) {
+            dvec2 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(q + (size_t)(s + u) * 64);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc += v[u];
+        }
+        for (; s < S; ++s) acc += __builtin_nontemporal_load(q + (size_t)s * 64);
+        dvec2 *o = out + (size_t)c * Wk * 64 + lane;
+        for (int w = 0; w < Wk; ++w) {
+            if (nt_store) __builtin_nontemporal_store(acc, o + (size_t)w * 64);
+            else o[(size_t)w * 64] = acc;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void front_kernel(const dvec2 *__restrict__ p, size_t n, double *sink)
 {
     dvec2 acc = {0, 0};
@@ -114,6 +142,19 @@ int main(int argc, char **argv)
                 if (U == 8) hipLaunchKernelGGL(chunk_kernel<8>, dim3(blocks), dim3(256), 0, 0, a, nchunks, S, G, sink);
             };
             printf(", \"U%d_G%d\": %.1f", U, G, timeit(go));
+        }
+    }
+    // small write fractions inside the read stream (per wave: S KiB read, Wk KiB written)
+    dvec2 *wout;
+    CK(hipMalloc(&wout, (size_t)nchunks * 4 * 1024));
+    for (int Wk : {0, 1, 2, 4}) {
+        for (int nt : {0, 1}) {
+            if (Wk == 0 && nt) continue;
+            auto go = [&] {
+                hipLaunchKernelGGL(chunk_write_kernel, dim3(blocks), dim3(256), 0, 0, a, wout, nchunks, S, Wk, nt);
+            };
+            const double rd = timeit(go); // GB/s of the read bytes alone
+            printf(", \"W%d%s_read_GBps\": %.1f", Wk, nt ? "nt" : "", rd);
         }
     }
     printf("}\n");

@@ -1032,6 +1032,20 @@ int df_get_field(df_handle *h, int which, double *out)
     return check_rng_error(h);
 }
 
+int df_set_field(df_handle *h, int which, const double *host_in)
+{
+    if (!valid_dev(h) || !host_in) return DF_EINVAL;
+    if (which < DF_U || which > DF_FILT_OLD_W) return fail(DF_EINVAL, "df_set_field: only u, v, w, T, rho and filt_old");
+    double *dst = const_cast<double *>(df_device_field(h, which));
+    if (!dst) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    int rc = sync_all(h); // a running call must not see half a field
+    if (rc) return rc;
+    HIP_OR(hipMemcpyAsync(dst, host_in, (size_t)h->Ny * h->Nz_loc * 8, hipMemcpyHostToDevice, h->stream), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return DF_OK;
+}
+
 const double *df_device_field(df_handle *h, int which)
 {
     if (!valid_dev(h)) return nullptr;

@@ -77,6 +77,7 @@ def lib():
         "df_get_rho_T_fluc": (C.c_int, [H]),
         "df_get_field": (C.c_int, [H, C.c_int, C.c_void_p]),
         "df_device_field": (C.c_void_p, [H, C.c_int]),
+        "df_set_field": (C.c_int, [H, C.c_int, C.c_void_p]),
         "df_dims": (C.c_int, [H] + [C.POINTER(C.c_int)] * 4),
         "df_get_row": (C.c_int, [H, C.c_int, C.c_void_p]),
         "df_get_scalar": (C.c_double, [H, C.c_int]),
@@ -240,6 +241,21 @@ class DigitalFilter:
 
     def fields(self):
         return {k: self.field(k) for k in ("u", "v", "w", "T", "rho")}
+
+    def set_field(self, name, values):
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        if a.size != self.Ny * self.Nz_loc:
+            raise DFError(f"set_field: need {self.Ny} x {self.Nz_loc} values")
+        _check(lib().df_set_field(self._h, FIELDS[name], a.ctypes.data))
+
+    def checkpoint(self):
+        """The resumable state: stream state and filt_old of u, v, w."""
+        return {"rng": self.rng_state(), **{k: self.field(k) for k in ("filt_old_u", "filt_old_v", "filt_old_w")}}
+
+    def restore(self, ck):
+        self.set_rng_state(*ck["rng"])
+        for k in ("filt_old_u", "filt_old_v", "filt_old_w"):
+            self.set_field(k, ck[k])
 
     def device_ptr(self, name):
         return lib().df_device_field(self._h, FIELDS[name])

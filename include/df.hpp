@@ -52,6 +52,16 @@ struct FilterField { // df.hpp:24-34
     int Nz_max = 0, Ny_max = 0;
 };
 
+// The reference's resumable state: the process-wide stream (df.cpp:334-335) and
+// filt_old of u, v, w (df.cpp:440-442). restore() on a handle of the same plane continues the
+// saved run bit for bit.
+struct DFCheckpoint {
+    std::uint64_t rng_state = 0;
+    int rng_saved_flag = 0;
+    double rng_saved = 0.0;
+    Vector filt_old_u, filt_old_v, filt_old_w;
+};
+
 struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     double d_i = 0.0013, rho_e = 0.044, U_e = 869.1, mu_e = 7.1212e-6;
     int vel_file_offset = 0, vel_file_N_values = 0;
@@ -444,5 +454,24 @@ class DIGITAL_FILTER {
     void rng_state(std::uint64_t &state, int &saved_flag, double &saved)
     {
         check(df_rng_state(h_, &state, &saved_flag, &saved));
+    }
+    DFCheckpoint checkpoint()
+    {
+        DFCheckpoint ck;
+        rng_state(ck.rng_state, ck.rng_saved_flag, ck.rng_saved);
+        pull(ck.filt_old_u, DF_FILT_OLD_U);
+        pull(ck.filt_old_v, DF_FILT_OLD_V);
+        pull(ck.filt_old_w, DF_FILT_OLD_W);
+        return ck;
+    }
+    void restore(const DFCheckpoint &ck)
+    {
+        for (const Vector *f : {&ck.filt_old_u, &ck.filt_old_v, &ck.filt_old_w})
+            if ((int)f->size() != n_cells) throw std::invalid_argument("checkpoint is for another plane");
+        check(df_set_rng_state(h_, ck.rng_state, ck.rng_saved_flag, ck.rng_saved));
+        check(df_set_field(h_, DF_FILT_OLD_U, ck.filt_old_u.data()));
+        check(df_set_field(h_, DF_FILT_OLD_V, ck.filt_old_v.data()));
+        check(df_set_field(h_, DF_FILT_OLD_W, ck.filt_old_w.data()));
+        refresh();
     }
 };

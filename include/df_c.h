@@ -124,6 +124,11 @@ int df_get_rho_T_fluc(df_handle *h);                /* df.cpp:470-485 */
 
 /* Host copy of a dense [Ny x Nz_local] field (u.fluc etc., df.hpp:24-34). Synchronizes. */
 int df_get_field(df_handle *h, int which, double *host_out);
+/* Upload a dense [Ny x Nz_local] host field into which = DF_U..DF_FILT_OLD_W. Synchronizes.
+ * Checkpoint/resume: the reference's resumable state is the stream (df_rng_state)
+ * plus filt_old of u, v, w (df.cpp:440-442); df_set_rng_state + df_set_field(DF_FILT_OLD_*)
+ * on any handle of the same plane makes its next df_filter continue the saved run bit for bit. */
+int df_set_field(df_handle *h, int which, const double *host_in);
 /* Device pointer of the same dense field (row-major, pitch Nz_local doubles). */
 const double *df_device_field(df_handle *h, int which);
 /* Ny, global Nz, and the [z0, z1) columns this handle owns. */

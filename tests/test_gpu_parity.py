@@ -368,3 +368,24 @@ def test_grid_plane_table_equals_packed_and_strips_equal_whole():
     for k in FIELDS:
         assert np.array_equal(a.field(k), b.field(k)), k
         assert np.array_equal(np.concatenate([s.field(k) for s in strips], axis=1), a.field(k)), k
+
+
+def test_checkpoint_restore_continues_bitexact():
+    """SURVEY 5 checkpoint/resume: stream state + filt_old x3 restored on another handle of the
+    same plane (itself at a different point of a different stream) continue the run exactly."""
+    spec = (96, 140, 2, 12)
+    a = gpu_synth(*spec, seed=5)
+    a.filter(1e-8)
+    ck = a.checkpoint()
+    for _ in range(2):
+        a.filter(2e-8)
+    b = gpu_synth(*spec, seed=99)
+    b.filter(1e-5)
+    b.restore(ck)
+    for _ in range(2):
+        b.filter(2e-8)
+    assert b.rng_state() == a.rng_state()
+    for k in FIELDS + ("filt_old_u", "filt_old_v", "filt_old_w"):
+        assert np.array_equal(a.field(k), b.field(k)), k
+    with pytest.raises(dfamd.DFError, match="need"):
+        b.set_field("filt_old_u", np.zeros(5))

@@ -136,6 +136,8 @@ def test_c_abi_rejects_bad_arguments():
     assert L.df_get_row(f._h, 99, (C.c_double * f.Ny)()) == -1
     assert L.df_get_coeffs(f._h, 0, 0, (C.c_double * 4)(), 4) == -1  # too small
     assert "too small" in L.df_last_error().decode()
+    assert L.df_set_field(f._h, 5, (C.c_double * 4)()) == -1  # host-only handle
+    assert b"host-only" in L.df_last_error()
     assert L.df_set_tuning(None, b"rows_per_wave", 2) == -1
     assert L.df_set_tuning(f._h, b"bogus", 2) == -1
     assert b"unknown tuning" in L.df_last_error()

@@ -218,6 +218,26 @@ template <class G> __device__ __forceinline__ StreamPos stream_pos(const G &g, u
     return {sidx, row, p - row * W};
 }
 
+// Position d normals further on (wave-uniform, SALU): at most two row steps when rows hold
+// >= 128 normals and d <= 128; sidx == 6 means past the end of the call's stream.
+template <class G> __device__ __forceinline__ StreamPos stream_advance(const G &g, StreamPos s, uint32_t d)
+{
+    while (d > 0 && s.sidx < 6) {
+        const uint32_t room = g.width[s.sidx] - s.col;
+        if (d < room) {
+            s.col += d;
+            break;
+        }
+        d -= room;
+        s.col = 0;
+        if (++s.row == g.rows[s.sidx]) {
+            s.row = 0;
+            ++s.sidx;
+        }
+    }
+    return s;
+}
+
 template <class G> __device__ __forceinline__ StreamPos stream_next(const G &g, StreamPos s)
 {
     if (++s.col == g.width[s.sidx]) {
@@ -390,6 +410,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     // recomputed only when one of its normals is stored (or it ends the call);
     // every other attempt just jumps the state to the thread's next attempt.
     uint64_t st = thread_first_state(g, sin->state, blockIdx.x, tid); // start of attempt m
+    // The wave's runs of iterations m, m+1, ... are consecutive in the stream (wave-major ranks),
+    // so its position is located once and then advanced by 2*n_acc per iteration.
+    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)(Ob + uniform(pre[0][w])));
     for (int m = 0; m < kRngPerThread; ++m) {
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
@@ -400,12 +423,12 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         const long long rank0 = Ob + uniform(pre[m][w]); // scalar: the wave-level math below runs on the SALU
         const int n_acc = __popcll(mask);
         const uint64_t q_first = f + 2ull * (uint64_t)rank0;
-        const uint64_t q_end = q_first + 2ull * (uint64_t)n_acc; // exclusive
-        // Wave-level position from the kernel-argument tables: q_first is uniform, so this
-        // runs on the SALU with scalar loads (the LDS copy T serves per-lane lookups only).
-        const StreamPos P0 = stream_pos(g, q_first);
-        const int su = uniform(P0.sidx);
-        const bool fast = n_acc > 0 && g.width[su] >= 2 * 64 && q_end <= g.seg[su + 1];
+        const StreamPos P0 = P; // == stream_pos(g, q_first)
+        P = stream_advance(g, P, 2u * (uint32_t)n_acc);
+        const int su = uniform(P0.sidx < 6 ? P0.sidx : 5);
+        // the run [q_first, q_first + 2*n_acc) stays inside array su (counts fit 32 bits: host check)
+        const uint32_t left = (g.rows[su] - P0.row) * g.width[su] - P0.col;
+        const bool fast = n_acc > 0 && P0.sidx < 6 && g.width[su] >= 2 * 64 && 2u * (uint32_t)n_acc <= left;
         // Wave-uniform skip (SALU): the run [q_first, q_end) stays in one row of one array and
         // every column it covers is one this GPU never stores (the r_zs interior, df.cpp:377,
         // or another strip's r_ys columns), and it does not hold the call's last attempt.

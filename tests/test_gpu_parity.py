@@ -389,3 +389,52 @@ def test_checkpoint_restore_continues_bitexact():
         assert np.array_equal(a.field(k), b.field(k)), k
     with pytest.raises(dfamd.DFError, match="need"):
         b.set_field("filt_old_u", np.zeros(5))
+
+
+# ---------------------------------------------------------------- randomized sweep of shapes
+
+def _random_cases(n=10, seed=20261015):
+    rng = np.random.default_rng(seed)
+    cases = []
+    for i in range(n):
+        kind = "grid" if i % 3 == 2 else "synthetic"
+        Ny = int(rng.integers(8, 90))
+        Nz = int(rng.integers(1, 300))
+        lo = int(rng.integers(1, 6)) * 2
+        hi = lo + int(rng.integers(0, 12)) * 2
+        mode = "table" if rng.random() < 0.4 else "packed"
+        rpw = int(rng.choice([0, 1, 2, 4, 8]))
+        world = int(rng.choice([1, 1, 2, 3])) if Nz >= 3 * (hi + 1) else 1
+        cases.append(dict(kind=kind, Ny=Ny, Nz=Nz, lo=lo, hi=hi, mode=mode, rpw=rpw, world=world,
+                          seed=int(rng.integers(0, 2**31)), phase=float(rng.random() * 6)))
+    return cases
+
+
+@pytest.mark.parametrize("case", _random_cases(), ids=lambda c: "{kind}-{Ny}x{Nz}-N{lo}-{hi}-{mode}-r{rpw}-w{world}".format(**c))
+def test_random_planes_vs_oracle(case):
+    c = case
+    if c["kind"] == "grid":
+        Ny, Nz = max(c["Ny"], 20), max(c["Nz"], 4)
+        gy, gz = O.warped_grid(Ny, Nz, dz0=3.0e-5, wave=0.15, seed_phase=c["phase"])
+        kw = dict(plane="grid", grid_y=gy, grid_z=gz)
+        o = O.Filter(plane=O.PLANE_GRID, Ny=Ny, Nz=Nz, grid_y=gy, grid_z=gz, seed=c["seed"])
+    else:
+        kw = dict(plane="synthetic", Ny=c["Ny"], Nz=c["Nz"], N_min=c["lo"], N_max=c["hi"])
+        o = oracle_synth(c["Ny"], c["Nz"], c["lo"], c["hi"], seed=c["seed"])
+    kw.update(device=0, seed=c["seed"], coeff_mode=c["mode"], rows_per_wave=c["rpw"])
+    try:
+        hs = dfamd.create_group(c["world"], **kw) if c["world"] > 1 else [dfamd.DigitalFilter(**kw)]
+    except dfamd.DFError as e:  # a z-strip narrower than the z half-width is refused by design
+        assert "narrower" in str(e)
+        return
+    for dt in (None, 1e-8, 3e-8):
+        if dt is not None:
+            if len(hs) > 1:
+                dfamd.filter_group(hs, dt)
+            else:
+                hs[0].filter(dt)
+            o.filter(dt)
+        assert all(h.rng_state() == o.rng.state for h in hs)
+        for k in FIELDS:
+            got = np.concatenate([h.field(k) for h in hs], axis=1)
+            assert float(rel_err(got, o.field(k)).max()) <= TOL, (dt, k)

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
 import torch  # noqa: E402,F401  (one HIP runtime per process, as bench.py)
 import dfamd  # noqa: E402
 
-CFG = {"c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64),
+CFG = {"c1": (128, 128, 8, 8), "c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64),
        "u64": (2048, 2048, 64, 64), "u16": (2048, 2048, 16, 16), "c3big": (4096, 2048, 4, 64)}
 
 

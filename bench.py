@@ -179,6 +179,7 @@ def main():
         f.close()
         g = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=args.seed,
                                 device=local_rank, coeff_mode=other, rows_per_wave=args.rows_per_wave)
+        taps = sum(g.comp_info(c)["by_size"] + g.comp_info(c)["bz_size"] for c in range(3))
         for _ in range(args.warmup):
             g.filter(args.dt)
         g.sync()
@@ -202,6 +203,16 @@ def main():
             alt[other]["note"] = ("same results bit for bit (tests/test_gpu_parity.py); coefficients read from a "
                                   "per-N table instead of the 20.7 GB offset-packed stream, so SURVEY 8d's "
                                   "algorithmic bytes do not apply: the roofline uses rocprofv3-measured bytes")
+            # Table mode is FP64-VALU bound: 2 flop (mul, add) per tap and cell (5.17 GFLOP at c3).
+            # Peak: MI355X FP64 vector 78.6 TFLOP/s (datasheet; half the guide's 157.3 FP32); the sums
+            # must not contract to FMA (bit-exactness), which caps mul+add at half of that.
+            sw_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
+            flops = 2.0 * taps
+            alt[other]["roofline_valu"] = {"bound": "valu-fp64", "achieved": round(flops / (sw_ms * 1e-3) / 1e12, 2),
+                                           "peak": 78.6, "unit": "TFLOP/s",
+                                           "frac": round(flops / (sw_ms * 1e-3) / 1e12 / 78.6, 4),
+                                           "flops_per_call": flops, "sweeps_ms": round(sw_ms, 4),
+                                           "note": "mul+add without FMA contraction caps at 39.3 TFLOP/s"}
             if all(m is not None for m in meas):
                 sweeps_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
                 ach = sum(meas) / (sweeps_ms * 1e-3) / 1e9

@@ -590,7 +590,7 @@ int build(df_handle *h, const df_config_c *cfg)
     // the memory-bound sweeps keep their waves; the compute-bound RNG fills gaps.
     int prio_lo = 0, prio_hi = 0;
     HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
-    int use_prio = 0; // measured: priorities cost 1-2% wall time (profiles/r1/ab_prio_*.json)
+    int use_prio = 0; // measured: priorities cost 1-2% wall time (in-process A/B, tools/ab.py)
     if (const char *e = std::getenv("DFAMD_RNG_PRIO")) use_prio = std::atoi(e);
     HIP_OR(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, use_prio ? prio_hi : 0), DF_EHIP);
     HIP_OR(hipStreamCreateWithPriority(&h->rng_stream, hipStreamNonBlocking, use_prio ? prio_lo : 0), DF_EHIP);

@@ -8,6 +8,7 @@ there is no CPU fallback: a missing library or GPU raises.
 """
 import ctypes as C
 import os
+import sys
 
 import numpy as np
 
@@ -208,6 +209,10 @@ class DigitalFilter:
             self._h = None
 
     def __del__(self):
+        # At interpreter exit the HIP runtime may already be torn down: leave the handle to
+        # process teardown then (call close() explicitly to release it earlier).
+        if sys is None or sys.is_finalizing():
+            return
         self.close()
 
     # --- hot path

@@ -200,12 +200,28 @@ class DIGITAL_FILTER {
         c.rng_saved = config.rng_saved;
         h_ = df_create(&c);
         if (!h_) throw std::runtime_error(std::string("DIGITAL_FILTER: ") + df_last_error());
+        try {
+            mirror_setup();
+        } catch (...) { // the destructor does not run for a half-built object
+            df_destroy(h_);
+            h_ = nullptr;
+            throw;
+        }
+    }
+    DIGITAL_FILTER(const DIGITAL_FILTER &) = delete;
+    DIGITAL_FILTER &operator=(const DIGITAL_FILTER &) = delete;
+    ~DIGITAL_FILTER() { df_destroy(h_); }
+
+  private:
+    // Host mirrors of the setup (rows, scalars, vertices, half-widths) and of step 0's fields.
+    void mirror_setup()
+    {
         int ny, nz, z0, z1;
         check(df_dims(h_, &ny, &nz, &z0, &z1));
         Ny = ny;
         Nz = z1 - z0;
         n_cells = Ny * Nz;
-        d_i = config.d_i;
+        d_i = cfg_.d_i;
         d_v = df_get_scalar(h_, 2);
         u_tau = df_get_scalar(h_, 0);
         tau_w = df_get_scalar(h_, 1);
@@ -236,10 +252,8 @@ class DIGITAL_FILTER {
         T_fluc.assign(n_cells, 0.0);
         refresh();
     }
-    DIGITAL_FILTER(const DIGITAL_FILTER &) = delete;
-    DIGITAL_FILTER &operator=(const DIGITAL_FILTER &) = delete;
-    ~DIGITAL_FILTER() { df_destroy(h_); }
 
+  public:
     // ====== setup steps: performed by the constructor (df.cpp:26-53); kept for API parity
     void read_grid() {}
     void allocate_data_structures(FilterField &F) { (void)comp_of(F); }

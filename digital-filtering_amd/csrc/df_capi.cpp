@@ -99,11 +99,13 @@ struct df_handle {
     long long *offsets = nullptr;
     long long *part = nullptr; // K2a run totals -> run prefixes (K2b)
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
+    int *wave_counts = nullptr; // accepted attempts per wave of each block (K1 -> K2c)
+    WaveTask *tasks = nullptr;  // waves K3 runs (K2c)
+    int *ntasks = nullptr;
     int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped
     int *err_host = nullptr;
     int rng_blocks = 0;       // attempt blocks per call (4096 attempts each), same on every rank
     int rng_chunk = 0;        // blocks counted by each z-strip rank (split counting, SURVEY 8e option A)
-    int own_b0 = 0, own_b1 = 0; // this rank's counted blocks
     bool split_count = false;
     ncclComm_t rng_comm = nullptr;           // second communicator: the count all-gather runs on rng_stream
     hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
@@ -258,9 +260,11 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     }
     const RngStateDev *in = h->rstate + (h->gen_launched & 1);
     if (!h->split_count)
-        HIP_OR(launch_rng_count(g, in, h->counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs), DF_EHIP);
+        HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs),
+               DF_EHIP);
     else
-        HIP_OR(launch_rng_count(g, in, h->counts, h->masks, h->rank * h->rng_chunk, h->rng_chunk, h->rng_blocks, rs),
+        HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, h->rank * h->rng_chunk, h->rng_chunk,
+                                h->rng_blocks, rs),
                DF_EHIP);
     return DF_OK;
 }
@@ -272,8 +276,8 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
     // every rank holds every block's accept masks (gathered with the counts), so K3 never
     // redraws accept decisions
     HIP_OR(launch_rng_finish(g, h->rstate + (h->gen_launched & 1), h->rstate + ((h->gen_launched + 1) & 1),
-                             h->counts, h->offsets, h->part, h->masks, h->err_dev, h->rng_blocks, nb_scan, 0,
-                             h->rng_blocks, rs),
+                             h->counts, h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks,
+                             h->err_dev, h->rng_blocks, nb_scan, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5);
     HIP_OR(hipEventRecord(h->ev_rng[set], rs), DF_EHIP);
@@ -307,6 +311,9 @@ int launch_gen_group(std::vector<df_handle *> &hs)
             HIP_OR(hipMemcpyAsync(h->masks + at * kRngThreads, hs[o]->masks + at * kRngThreads,
                                   (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t), hipMemcpyDefault, rss[r]),
                    DF_EHIP);
+            HIP_OR(hipMemcpyAsync(h->wave_counts + at * kWavesPerBlock, hs[o]->wave_counts + at * kWavesPerBlock,
+                                  (size_t)h->rng_chunk * kWavesPerBlock * sizeof(int), hipMemcpyDefault, rss[r]),
+                   DF_EHIP);
         }
         if ((rc = gen_end(h, gs[r], rss[r]))) return rc;
     }
@@ -328,9 +335,12 @@ int launch_gen(df_handle *h)
         int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
         const size_t mbytes = (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t);
         uint16_t *mmine = h->masks + (size_t)h->rank * h->rng_chunk * kRngThreads;
-        if (h->rng_comm) { // the RNG's one exchange: per-block accept counts and masks
+        const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
+        int *wmine = h->wave_counts + (size_t)h->rank * nwc;
+        if (h->rng_comm) { // the RNG's one exchange: accept counts (block, wave) and masks
             NCCL_OR(ncclGroupStart());
             NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
+            NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
             NCCL_OR(ncclAllGather(mmine, h->masks, mbytes, ncclUint8, h->rng_comm, rs));
             NCCL_OR(ncclGroupEnd());
         } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
@@ -340,6 +350,9 @@ int launch_gen(df_handle *h)
                                           hipMemcpyDeviceToDevice, rs),
                            DF_EHIP);
                     HIP_OR(hipMemcpyAsync(h->masks + (size_t)o * h->rng_chunk * kRngThreads, mmine, mbytes,
+                                          hipMemcpyDeviceToDevice, rs),
+                           DF_EHIP);
+                    HIP_OR(hipMemcpyAsync(h->wave_counts + (size_t)o * nwc, wmine, nwc * sizeof(int),
                                           hipMemcpyDeviceToDevice, rs),
                            DF_EHIP);
                 }
@@ -712,13 +725,14 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = dalloc_t(h, &h->rstate, 2))) return rc;
     h->rng_chunk = (h->rng_blocks + h->world - 1) / h->world;
     const int nb_pad = h->rng_chunk * h->world;
-    h->own_b0 = std::min(h->rank * h->rng_chunk, h->rng_blocks);
-    h->own_b1 = std::min(h->own_b0 + h->rng_chunk, h->rng_blocks);
     if ((rc = dalloc_t(h, &h->counts, nb_pad))) return rc;
     if ((rc = dalloc_t(h, &h->offsets, nb_pad))) return rc;
     if ((nb_pad + 1023) / 1024 > 1024) return fail(DF_EINVAL, "plane too large for the RNG scan (> 2^20 attempt blocks)");
     if ((rc = dalloc_t(h, &h->part, (nb_pad + 1023) / 1024))) return rc;
     if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
+    if ((rc = dalloc_t(h, &h->wave_counts, (size_t)nb_pad * kWavesPerBlock))) return rc;
+    if ((rc = dalloc_t(h, &h->tasks, (size_t)nb_pad * kWavesPerBlock))) return rc;
+    if ((rc = dalloc_t(h, &h->ntasks, 1))) return rc;
     HIP_OR(hipEventCreateWithFlags(&h->ev_counted, hipEventDisableTiming), DF_EHIP);
     {
         // jump tables: block b starts 4*4096*b outputs in; thread tid = 64*w + l starts

@@ -102,14 +102,15 @@ __device__ __forceinline__ uint64_t thread_first_state(const RngGeom &g, uint64_
 // Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
 // the last z-strip rank's share) report zero.
 __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                               int *__restrict__ counts,
+                                                               int *__restrict__ counts, int *__restrict__ wave_counts,
                                                                uint16_t *__restrict__ masks, int b0, int nb_total)
 {
     __shared__ int wsum[kRngThreads / 64];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, w = tid >> 6;
     const int gb = b0 + blockIdx.x;
     if (gb >= nb_total) {
         if (tid == 0) counts[gb] = 0;
+        if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
         return;
     }
     uint64_t st = thread_first_state(g, sin->state, gb, tid);
@@ -124,11 +125,14 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
     }
     masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if ((tid & 63) == 0) wsum[tid >> 6] = cnt;
+    if ((tid & 63) == 0) {
+        wsum[w] = cnt;
+        wave_counts[(size_t)gb * (kRngThreads / 64) + w] = cnt; // the wave's run of 1024 attempts
+    }
     __syncthreads();
     if (tid == 0) {
         int t = 0;
-        for (int w = 0; w < kRngThreads / 64; ++w) t += wsum[w];
+        for (int ww = 0; ww < kRngThreads / 64; ++ww) t += wsum[ww];
         counts[gb] = t;
     }
 }
@@ -169,10 +173,11 @@ __global__ __launch_bounds__(256) void rng_scan_local_kernel(const int *__restri
 
 __global__ __launch_bounds__(1024) void rng_scan_parts_kernel(long long *__restrict__ part, int nparts,
                                                               const RngStateDev *__restrict__ sin, uint64_t Q,
-                                                              int *__restrict__ err)
+                                                              int *__restrict__ err, int *__restrict__ ntasks)
 {
     __shared__ long long p[1024];
     const int tid = threadIdx.x;
+    if (tid == 0) *ntasks = 0; // K2c appends this call's wave tasks
     p[tid] = tid < nparts ? part[tid] : 0;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {
@@ -189,17 +194,6 @@ __global__ __launch_bounds__(1024) void rng_scan_parts_kernel(long long *__restr
     }
 }
 
-// The stream-layout tables of RngGeom, staged in LDS by the generate kernel:
-// indexing kernel arguments with a per-lane array index compiles to global
-// loads (and vmcnt stalls) inside the hot loop; LDS reads do not.
-struct StreamTables {
-    uint64_t seg[7];
-    uint64_t inv_width[6];
-    uint32_t width[6], rows[6];
-    double *ry[3], *rz[3];
-    int Nzp[3], rz_pitch[3];
-    int Nz_g, Pz, z0, z1, is_first, is_last;
-};
 
 // A stream position q as (array, row, column) of the reference's six arrays.
 struct StreamPos {
@@ -307,112 +301,72 @@ template <class G> __device__ bool range_needed(const G &g, uint64_t q0, uint64_
     return false;
 }
 
-__global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                                  RngStateDev *__restrict__ sout,
-                                                                  const long long *__restrict__ offsets,
-                                                                  const long long *__restrict__ part,
-                                                                  const uint16_t *__restrict__ masks,
-                                                                  const int *__restrict__ counts, int own_b0,
-                                                                  int own_b1)
+// K2c: one thread per wave of attempts (4 per block). A wave's accepted attempts hold ranks
+// [r_lo, r_hi) = block offset + the preceding waves' counts, i.e. stream positions
+// [f + 2 r_lo, f + 2 r_hi). Waves that store something on this GPU (or end the call) are
+// appended to a task list, so K3 never runs a wave that only feeds other strips or the r_zs
+// interior. Also stores the cached normal carried into the call (stream position 0).
+__global__ __launch_bounds__(256) void rng_plan_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                       const long long *__restrict__ offsets,
+                                                       const long long *__restrict__ part,
+                                                       const int *__restrict__ wave_counts, int nb_total,
+                                                       WaveTask *__restrict__ tasks, int *__restrict__ ntasks)
 {
-    __shared__ int cnt[kRngPerThread][kRngThreads / 64];
-    __shared__ int pre[kRngPerThread][kRngThreads / 64];
-    __shared__ StreamTables T;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr int WPB = kRngThreads / 64; // waves per attempt block
+    const int gw = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
-    const long long Ob = offsets[blockIdx.x] + part[blockIdx.x >> 10];
-    const bool own = (int)blockIdx.x >= own_b0 && (int)blockIdx.x < own_b1;
-    // issued early: its latency overlaps the block-level tests below
-    const uint32_t own_bits = own ? masks[(size_t)blockIdx.x * kRngThreads + tid] : 0u;
-    if (Ob >= A) return; // uniform: the whole block is past the call's last attempt
-    {
-        // Blocks whose normals all land on other GPUs' columns (or in the r_zs
-        // interior) have nothing to store; the one holding the last accepted
-        // attempt still records the stream state.
-        const long long Oe = Ob + counts[blockIdx.x];
-        const uint64_t q_lo = f + 2ull * (uint64_t)Ob;
-        const uint64_t q_hi = (f + 2ull * (uint64_t)Oe) < g.Q ? (f + 2ull * (uint64_t)Oe) : g.Q;
-        const bool holds_last = Oe >= A;
-        if (!holds_last && !(blockIdx.x == 0 && f) && !range_needed(g, q_lo, q_hi)) return;
-    }
-    if (tid < 7) T.seg[tid] = g.seg[tid];
-    if (tid >= 64 && tid < 70) {
-        const int i = tid - 64;
-        T.inv_width[i] = g.inv_width[i];
-        T.width[i] = g.width[i];
-        T.rows[i] = g.rows[i];
-    }
-    if (tid >= 128 && tid < 131) {
-        const int c = tid - 128;
-        T.ry[c] = g.ry[c];
-        T.rz[c] = g.rz[c];
-        T.Nzp[c] = g.Nzp[c];
-        T.rz_pitch[c] = g.rz_pitch[c];
-    }
-    if (tid == 192) {
-        T.Nz_g = g.Nz_g;
-        T.Pz = g.Pz;
-        T.z0 = g.z0;
-        T.z1 = g.z1;
-        T.is_first = g.is_first;
-        T.is_last = g.is_last;
-    }
-    __syncthreads();
-
-    if (blockIdx.x == 0 && tid == 0 && f) {
-        double *d = stream_dest(T, stream_pos(T, 0));
+    if (gw == 0 && f) {
+        double *d = stream_dest(g, stream_pos(g, 0));
         if (d) *d = sin->saved * 1.0 + 0.0;
     }
-    uint32_t bits;
-    if (own) {
-        bits = own_bits; // K1's accept flags (this rank's count, or gathered from the others)
-    } else { // accept flags not available here: redo the tests
-        bits = 0;
-        uint64_t sc = thread_first_state(g, sin->state, blockIdx.x, tid);
-        for (int m = 0; m < kRngPerThread; ++m) {
-            bits |= (polar_attempt(sc).accept ? 1u : 0u) << m;
-            sc = g.hop_mult * sc + g.hop_plus;
+    bool need = false;
+    long long r_lo = 0;
+    if (gw < nb_total * WPB) {
+        const int b = gw / WPB, w = gw % WPB;
+        r_lo = offsets[b] + part[b >> 10];
+        for (int ww = 0; ww < w; ++ww) r_lo += wave_counts[(size_t)b * WPB + ww];
+        const long long r_hi = r_lo + wave_counts[gw];
+        if (r_lo < A) {
+            const uint64_t q_lo = f + 2ull * (uint64_t)r_lo;
+            const uint64_t q_hi = (f + 2ull * (uint64_t)r_hi) < g.Q ? (f + 2ull * (uint64_t)r_hi) : g.Q;
+            const bool ends_call = A - 1 < r_hi;
+            need = ends_call || (q_lo < q_hi && range_needed(g, q_lo, q_hi));
         }
     }
-#pragma unroll
-    for (int m = 0; m < kRngPerThread; ++m) {
-        const uint64_t mask = __ballot((bits >> m) & 1u);
-        if (lane == 0) cnt[m][w] = __popcll(mask);
+    const uint64_t m = __ballot(need);
+    if (!m) return;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(ntasks, __popcll(m)); // one atomic per plan wave
+    base = __shfl(base, 0);
+    if (need) {
+        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        tasks[base + below] = WaveTask{r_lo, gw, 0};
     }
-    __syncthreads();
-    static_assert(kRngPerThread * (kRngThreads / 64) == 64, "one wave scans the block's (wave, m) counts");
-    if (w == 0) { // ranks in attempt order, wave-major (each wave owns a contiguous run): entry
-                  // e = 16*wave + m, one lane each, exclusive scan by shuffles
-        const int m = lane % kRngPerThread, ww = lane / kRngPerThread;
-        const int v = cnt[m][ww];
-        int x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(x, o);
-            if (lane >= o) x += y;
-        }
-        pre[m][ww] = x - v;
-    }
-    __syncthreads();
-    {
-        // The wave's accepted attempts own stream positions [f + 2*r_lo, f + 2*r_hi): a wave
-        // whose range stores nothing here (other strips' columns, the r_zs interior) and does
-        // not end the call has no pass 2 at all.
-        const long long r_lo = Ob + uniform(pre[0][w]);
-        const long long r_hi = Ob + uniform(pre[kRngPerThread - 1][w] + cnt[kRngPerThread - 1][w]);
-        const uint64_t q_lo = f + 2ull * (uint64_t)r_lo;
-        const uint64_t q_hi = (f + 2ull * (uint64_t)r_hi) < g.Q ? (f + 2ull * (uint64_t)r_hi) : g.Q;
-        const bool ends_call = r_lo <= A - 1 && A - 1 < r_hi;
-        if (r_lo >= A || (!ends_call && (q_lo >= q_hi || !range_needed(g, q_lo, q_hi)))) return;
-    }
-    // Pass 2: ranks come from the K1 accept flags, so an attempt's draws are
-    // recomputed only when one of its normals is stored (or it ends the call);
-    // every other attempt just jumps the state to the thread's next attempt.
-    uint64_t st = thread_first_state(g, sin->state, blockIdx.x, tid); // start of attempt m
+}
+
+// K3: one wave per task. Ranks come from K1's accept flags, so an attempt's draws are recomputed
+// only when one of its normals is stored (or it ends the call); every other attempt just jumps
+// the state to the lane's next attempt. Slots beyond the task count exit at once.
+__global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                  RngStateDev *__restrict__ sout,
+                                                                  const WaveTask *__restrict__ tasks,
+                                                                  const int *__restrict__ ntasks,
+                                                                  const uint16_t *__restrict__ masks)
+{
+    const int lane = threadIdx.x & 63;
+    const int slot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    if (slot >= *ntasks) return;
+    const int gw = uniform(tasks[slot].gw);
+    long long rank_w = tasks[slot].r_lo; // uniform
+    const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
+    const uint32_t bits = masks[(size_t)b * kRngThreads + tid];
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    uint64_t st = thread_first_state(g, sin->state, b, tid); // start of attempt m
     // The wave's runs of iterations m, m+1, ... are consecutive in the stream (wave-major ranks),
     // so its position is located once and then advanced by 2*n_acc per iteration.
-    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)(Ob + uniform(pre[0][w])));
+    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)rank_w);
     for (int m = 0; m < kRngPerThread; ++m) {
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
@@ -420,8 +374,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
         // [q_first, q_first + 2*n_acc): locate q_first once per wave; a lane's
         // position is then q_first + 2*below, at most one row wrap away when
         // the run stays inside one array and rows hold >= 128 normals.
-        const long long rank0 = Ob + uniform(pre[m][w]); // scalar: the wave-level math below runs on the SALU
         const int n_acc = __popcll(mask);
+        const long long rank0 = rank_w; // the wave's first rank in this iteration (uniform)
+        rank_w += n_acc;
         const uint64_t q_first = f + 2ull * (uint64_t)rank0;
         const StreamPos P0 = P; // == stream_pos(g, q_first)
         P = stream_advance(g, P, 2u * (uint32_t)n_acc);
@@ -470,9 +425,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
                     d0 = stream_dest(g, p0);
                     d1 = stream_dest(g, p1);
                 } else {
-                    const StreamPos p0 = stream_pos(T, q0);
-                    d0 = stream_dest(T, p0);
-                    d1 = (q0 + 1 < g.Q) ? stream_dest(T, stream_next(T, p0)) : nullptr;
+                    const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
+                    d0 = stream_dest(g, p0);
+                    d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
                 }
                 const bool last = (rank == A - 1);
                 if (d0 || d1 || last) {
@@ -513,22 +468,26 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     }
 }
 
-hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, uint16_t *masks, int b0,
-                            int nb, int nb_total, hipStream_t st)
+hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
+                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
-    hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, masks, b0, nb_total);
+    hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
+                       nb_total);
     return hipGetLastError();
 }
 
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                             long long *offsets, long long *part, uint16_t *masks, int *err, int nb_total,
-                             int nb_scan, int own_b0, int own_b1, hipStream_t st)
+                             const int *wave_counts, long long *offsets, long long *part, uint16_t *masks,
+                             WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st)
 {
     const int nparts = (nb_scan + 1023) / 1024; // <= 1024: checked at create
     hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
-    hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err);
-    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, st_out, offsets,
-                       part, masks, counts, own_b0, own_b1);
+    hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err, ntasks);
+    const int nw = nb_total * (kRngThreads / 64);
+    hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part, wave_counts,
+                       nb_total, tasks, ntasks);
+    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, st_out, tasks, ntasks,
+                       masks);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ constexpr int kStrip = 128;           // cells per strip (one wave, 2 per lane)
 constexpr int kRngThreads = 256;      // threads per RNG block
 constexpr int kRngPerThread = 16;     // polar attempts per thread
 constexpr int kRngBlockAttempts = kRngThreads * kRngPerThread;
+constexpr int kWavesPerBlock = kRngThreads / 64;
 static_assert(kRngThreads == 256 && kRngPerThread * 64 == kRngBlockAttempts / 4,
               "RNG mapping: 4 waves per block, each owning a contiguous run of 64 * kRngPerThread attempts");
 
@@ -36,6 +37,13 @@ struct RngStateDev {
 
 struct PcgJumpDev {
     uint64_t mult, plus;
+};
+
+// One wave of attempts whose normals this GPU stores (K2c -> K3): its first rank and its index
+// gw = 4 * block + wave.
+struct WaveTask {
+    long long r_lo;
+    int gw, pad;
 };
 
 struct RngGeom {
@@ -87,13 +95,11 @@ hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st
                                 const double *tab, const int *tab_off, int Ny, int nstrips, int Nz_loc,
                                 hipStream_t st);
 // K1 for blocks [b0, b0+nb) of nb_total (a z-strip rank counts its share only).
-hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, uint16_t *masks, int b0,
-                            int nb, int nb_total, hipStream_t st);
-// K2 + K3 once every block's count is present; blocks outside [own_b0, own_b1)
-// re-derive their accept flags.
+hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
+                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st);
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
-                             long long *offsets, long long *part, uint16_t *masks, int *err, int nb_total,
-                             int nb_scan, int own_b0, int own_b1, hipStream_t st);
+                             const int *wave_counts, long long *offsets, long long *part, uint16_t *masks,
+                             WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st);
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st);
 hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
 // Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),

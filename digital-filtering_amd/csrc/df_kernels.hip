@@ -118,9 +118,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
     uint32_t bits = 0;
 #pragma unroll 4
     for (int m = 0; m < kRngPerThread; ++m) {
-        PolarAttempt a = polar_attempt(st);
-        cnt += a.accept ? 1 : 0;
-        bits |= (a.accept ? 1u : 0u) << m;
+        const bool acc = polar_accept(st);
+        cnt += acc ? 1 : 0;
+        bits |= (acc ? 1u : 0u) << m;
         st = g.hop_mult * st + g.hop_plus;
     }
     masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3

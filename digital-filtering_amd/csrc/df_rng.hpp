@@ -95,4 +95,27 @@ DF_HD PolarAttempt polar_attempt(uint64_t &state)
     return a;
 }
 
+// The accept decision of polar_attempt alone (K1). A float screen from the high words decides
+// all but the attempts within 1e-5 of the unit circle or of the origin, which take the exact
+// double test: |xf - x| <= 2^-24*2 (fl(hi)) + 2^-24 (subtract) + 2^-31 (dropped lo) < 1.9e-7, so
+// |r2f - r2| < 2*2*1.9e-7 + 3 float roundings of values <= 2 < 1.2e-6.
+DF_HD bool polar_accept(uint64_t &state)
+{
+    uint32_t o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        o[i] = pcg_output(state);
+        state = state * kPcgMult + kPcgInc;
+    }
+    const float xf = (float)o[1] * 4.656612873077392578125e-10f - 1.0f; // 2^-31
+    const float yf = (float)o[3] * 4.656612873077392578125e-10f - 1.0f;
+    const float r2f = xf * xf + yf * yf;
+    if (r2f > 1e-5f && r2f < 1.0f - 1e-5f) return true;
+    if (r2f > 1.0f + 1e-5f) return false;
+    const double x = 2.0 * canonical_from(o[0], o[1]) - 1.0;
+    const double y = 2.0 * canonical_from(o[2], o[3]) - 1.0;
+    const double r2 = x * x + y * y;
+    return !(r2 > 1.0 || r2 == 0.0);
+}
+
 } // namespace dfamd

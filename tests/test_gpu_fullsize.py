@@ -164,10 +164,14 @@ def test_c5_full_size_sampled_rows():
 
 @pytest.mark.parametrize("spec", [dict(Ny=16, Nz=300, N_min=2, N_max=64),  # stencil far taller than the plane
                                   dict(Ny=300, Nz=3, N_min=2, N_max=40),   # 3 columns, z-stencil >> Nz
-                                  dict(Ny=64, Nz=129, N_min=2, N_max=2)])  # one column past a strip
+                                  dict(Ny=64, Nz=129, N_min=2, N_max=2),   # one column past a strip
+                                  dict(Ny=360, Nz=300, N_min=4, N_max=160, coeff_mode="table"),
+                                  dict(Ny=360, Nz=300, N_min=4, N_max=160)])  # halo wider than a 128-cell strip
 def test_extreme_aspect_planes(spec):
     seed = 11
-    g = dfamd.DigitalFilter(plane="synthetic", seed=seed, device=0, **spec)
+    spec = dict(spec)
+    mode = spec.pop("coeff_mode", "packed")
+    g = dfamd.DigitalFilter(plane="synthetic", seed=seed, device=0, coeff_mode=mode, **spec)
     o = O.Filter(plane=O.PLANE_SYNTHETIC, seed=seed, **spec)
     for dt in (None, 1e-8, 1e-8):
         if dt is not None:

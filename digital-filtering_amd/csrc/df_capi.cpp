@@ -86,13 +86,14 @@ struct df_handle {
     int rows_per_wave = 8;
     int nt_loads = 1; // coefficient stream is read once per call: non-temporal (measured +6%)
     int heavy_first = 1;
-    int yunroll = 2, zunroll = 4;
-    int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call) // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
+    int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
+    int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
+    int zstage = 1;    // table z-pass noise staged in LDS
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
     CompDev c[3];
-    double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr;
-    int *tab_off = nullptr;
+    double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr, *tabf = nullptr;
+    int *tab_off = nullptr, *tabf_off = nullptr;
     // RNG
     RngStateDev *rstate = nullptr; // [2], ping-pong by call parity
     int *counts = nullptr;
@@ -181,6 +182,8 @@ SweepArgs sweep_args(df_handle *h)
     a.nstrips = h->nstrips;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
+    a.tabf = h->tabf;
+    a.tabf_off = h->tabf_off;
     a.T = h->T;
     a.rho = h->rho;
     a.rowc = h->rowc;
@@ -191,6 +194,10 @@ SweepArgs sweep_args(df_handle *h)
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
     a.per_cell = h->setup.per_cell;
+    int nzp = 0;
+    for (int c = 0; c < 3; ++c) nzp = std::max(nzp, a.Nzp[c]);
+    a.zstage_reg = 4 * kStrip + 2 * nzp;
+    a.zstage = h->zstage && 3 * a.zstage_reg * (int)sizeof(double) <= 64 * 1024;
     return a;
 }
 
@@ -627,11 +634,27 @@ int build(df_handle *h, const df_config_c *cfg)
         tab_h.insert(tab_h.end(), kv.second.begin(), kv.second.end());
         tab_h.resize(tab_h.size() + (L - kv.second.size()), 0.0);
     }
+    // The same coefficients as full symmetric vectors b[|i|], i = -N..N, each starting on a
+    // 64-B boundary: a wave-uniform run of 8 taps is then one aligned s_load_dwordx16 with
+    // no |i| address arithmetic (row-uniform N: every non-grid plane).
+    std::vector<int> tabf_off_h(Nmax_all + 1, 0);
+    std::vector<double> tabf_h;
+    for (auto &kv : s.coeffs) {
+        tabf_h.resize((tabf_h.size() + 7) / 8 * 8, 0.0);
+        tabf_off_h[kv.first] = (int)tabf_h.size();
+        const int n = kv.first;
+        for (int i = -n; i <= n; ++i) tabf_h.push_back(kv.second[i < 0 ? -i : i]);
+    }
+    tabf_h.resize(tabf_h.size() + 8, 0.0);
     int rc;
     if ((rc = dalloc_t(h, &h->tab, tab_h.size()))) return rc;
     if ((rc = dalloc_t(h, &h->tab_off, tab_off_h.size()))) return rc;
     if ((rc = upload(h, h->tab, tab_h.data(), tab_h.size()))) return rc;
     if ((rc = upload(h, h->tab_off, tab_off_h.data(), tab_off_h.size()))) return rc;
+    if ((rc = dalloc_t(h, &h->tabf, tabf_h.size()))) return rc;
+    if ((rc = dalloc_t(h, &h->tabf_off, tabf_off_h.size()))) return rc;
+    if ((rc = upload(h, h->tabf, tabf_h.data(), tabf_h.size()))) return rc;
+    if ((rc = upload(h, h->tabf_off, tabf_off_h.data(), tabf_off_h.size()))) return rc;
 
     // ---- row constants of apply_RST_scaling / get_rho_T_fluc (df.cpp:425-438, 474)
     std::vector<double> rowc(7 * (size_t)Ny);
@@ -1222,6 +1245,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "yunroll") h->yunroll = value >= 4 ? 4 : 2;
     else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = value != 0;
+    else if (k == "zstage") h->zstage = value != 0;
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else return fail(DF_EINVAL, "unknown tuning key: " + k);
     return DF_OK;

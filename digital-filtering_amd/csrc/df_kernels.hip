@@ -22,14 +22,21 @@ __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirs
 // Timing-only ablations (Makefile `variant`): DF_ABLATE_NOISE replaces every noise load
 // of the sweeps by a register value, DF_ABLATE_COEF every coefficient load. Results are
 // wrong by design; the product is never built with either.
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(3))) dvec2 *lds_pair_ptr; // LDS-staged noise (ds_read_b128)
+__device__ __forceinline__ double2 ld_pair(const double2 *p) { return *p; }
+__device__ __forceinline__ double2 ld_pair(lds_pair_ptr p)
+{
+    const dvec2 v = *p;
+    return make_double2(v.x, v.y);
+}
 #if defined(DF_ABLATE_NOISE)
 #define DF_NOISE(ptr, tag) make_double2((double)(tag), (double)(threadIdx.x & 63))
 #else
-#define DF_NOISE(ptr, tag) (*(ptr))
+#define DF_NOISE(ptr, tag) ld_pair(ptr)
 #endif
 
 // Coefficient stream load: read once per call, so optionally non-temporal.
-typedef double dvec2 __attribute__((ext_vector_type(2)));
 template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
 {
 #if defined(DF_ABLATE_COEF)
@@ -540,7 +547,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
                 tb[r] = a.tab + a.tab_off[col < a.Nz_loc ? nc[col] : 0];
                 tb1[r] = a.tab + a.tab_off[col + 1 < a.Nz_loc ? nc[col + 1] : 0];
             } else if (TABLE) {
-                tb[r] = a.tab + a.tab_off[N[r]];
+                tb[r] = a.tabf + a.tabf_off[N[r]] + N[r]; // centre of the full vector: tap i at tb[i]
             } else {
                 bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + r] + (ptrdiff_t)(N[r] - r) * kStrip + 2 * lane;
             }
@@ -554,10 +561,13 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 
     auto coef = [&](int r, int t) -> double2 {
         if (TABLE) {
-            const int i = t - r, ai = i < 0 ? -i : i;
-            if (PC) return make_double2(tb[r][ai], tb1[r][ai]);
-            const double b = tb[r][ai];
-            return make_double2(b, b);
+            const int i = t - r;
+            if (!PC) {
+                const double b = tb[r][i];
+                return make_double2(b, b);
+            }
+            const int ai = i < 0 ? -i : i;
+            return make_double2(tb[r][ai], tb1[r][ai]);
         }
         return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
     };
@@ -667,6 +677,7 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 template <bool TABLE, bool NT, int ZU, bool PC>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
+    extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
     const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int Ny = a.Ny;
@@ -676,13 +687,42 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
     if (a.heavy_first) j = Ny - 1 - j;
     const int col = s * kStrip + 2 * lane;
 
+    // Table mode, the block's 4 tiles on one row with one tap range per component: the
+    // block stages that row's noise (512 + 2N columns per component) in LDS once and
+    // the waves read their tap pairs from there (ds_read_b128) instead of 4 overlapping
+    // (128 + 2N)-column windows through L1. Block-uniform: the barrier is reached by all.
+    bool staged = false;
+    if (TABLE && !PC && a.zstage) {
+        const int t0 = blockIdx.x * 4;
+        staged = t0 + 3 < a.nstrips * Ny && t0 / a.nstrips == (t0 + 3) / a.nstrips;
+        const int s0 = t0 - (t0 / a.nstrips) * a.nstrips;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            if (!staged || !((a.comps_mask >> c) & 1)) continue;
+            const int *ns = a.Nz_st[c] + (size_t)s0 * Ny + j;
+            const int N0 = ns[0];
+            staged = ns[Ny] == N0 && ns[2 * Ny] == N0 && ns[3 * Ny] == N0;
+        }
+        if (staged) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                if (!((a.comps_mask >> c) & 1)) continue;
+                const int N = a.Nz_st[c][(size_t)s0 * Ny + j];
+                const double *src = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + s0 * kStrip - N;
+                double *dst = zstage_lds + c * a.zstage_reg;
+                for (int e = threadIdx.x; e < 4 * kStrip + 2 * N; e += 256) dst[e] = src[e];
+            }
+            __syncthreads();
+        }
+    }
+
     double f0[3], f1[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         f0[c] = f1[c] = 0.0;
         if (!((a.comps_mask >> c) & 1)) continue;
         const int N = a.Nz_st[c][(size_t)s * Ny + j];
-        const double2 *xp = reinterpret_cast<const double2 *>(a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col - N);
+        const double2 *gxp = reinterpret_cast<const double2 *>(a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col - N);
         const double *bp = TABLE ? nullptr : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + 2 * lane; // tap t = i + N
         const double *tb = nullptr, *tb1 = nullptr;
         if (TABLE && PC) { // per-lane N; the table is zero past each N (taps up to N_st)
@@ -690,21 +730,28 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             tb = a.tab + a.tab_off[col < a.Nz_loc ? nc[col] : 0];
             tb1 = a.tab + a.tab_off[col + 1 < a.Nz_loc ? nc[col + 1] : 0];
         } else if (TABLE) {
-            tb = a.tab + a.tab_off[N];
+            tb = a.tabf + a.tabf_off[N]; // full vector: tap t at tb[t]
         }
         auto coef = [&](int t) -> double2 {
             if (TABLE) {
+                if (!PC) {
+                    const double v = tb[t];
+                    return make_double2(v, v);
+                }
                 const int i = t - N, ai = i < 0 ? -i : i;
-                if (PC) return make_double2(tb[ai], tb1[ai]);
-                const double v = tb[ai];
-                return make_double2(v, v);
+                return make_double2(tb[ai], tb1[ai]);
             }
             return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
         };
+        // one instantiation per address space: global (plain loads) or LDS (ds_read_b128)
+        auto taps = [&](auto xp, double &r0, double &r1) {
         double acc0 = 0.0, acc1 = 0.0;
         double2 P = DF_NOISE(xp, 0);
         int m = 0;
         if (ZU >= 4) {
+#if defined(DF_ZPASS_UNROLL1)
+#pragma unroll 1
+#endif
             for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
                 const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2), P3 = DF_NOISE(xp + m + 3, m + 3), P4 = DF_NOISE(xp + m + 4, m + 4);
                 double2 b[8];
@@ -754,8 +801,14 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         const double2 bl = coef(2 * N);
         acc0 += bl.x * P.x;
         acc1 += bl.y * P.y;
-        f0[c] = acc0;
-        f1[c] = acc1;
+        r0 = acc0;
+        r1 = acc1;
+        };
+        if (TABLE && !PC && staged) {
+            taps((lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane), f0[c], f1[c]);
+        } else {
+            taps(gxp, f0[c], f1[c]);
+        }
     }
 
     if (a.write_filt) {
@@ -841,8 +894,9 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
     if (table && a.per_cell) {
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), 0, st, a);
+        const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
     } else if (a.nt_loads) {
         if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);

@@ -76,6 +76,9 @@ struct SweepArgs {
     // coefficient table (DF_COEFF_TABLE mode): half-vector of N at tab + tab_off[N]
     const double *tab;
     const int *tab_off;
+    // the same as full symmetric vectors (b[|i|], i = -N..N) at tabf + tabf_off[N], 64-B aligned
+    const double *tabf;
+    const int *tabf_off;
     // z-pass epilogue
     double *filt_old[3], *fluc[3], *filt[3], *T, *rho;
     const double *rowc;     // 7 x Ny: sqrt(R11), b, sqrt(R22-b^2), sqrt(R33), SRA t1, Ts, rhos
@@ -84,8 +87,10 @@ struct SweepArgs {
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
     int nt_loads;           // non-temporal loads for the coefficient stream
     int heavy_first;        // schedule rows with the widest stencils first
-    int yunroll, zunroll;
-    int nt_stores;                        // sweep outputs stored non-temporally   // taps per loop iteration (tuning knobs)
+    int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
+    int nt_stores;          // sweep outputs stored non-temporally
+    int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
+    int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
 };
 
 // Launchers (all asynchronous on `st`). Return hipSuccess or the launch error.

@@ -222,6 +222,22 @@ def test_runtime_tuning_is_bitexact(mode):
         b.set_tuning("rows_per_wave", 3)
 
 
+@pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90)])
+def test_table_lds_staging_is_bitexact(spec):
+    # 6 and 9 strips: some blocks hold 4 strips of one row (noise staged in LDS), others
+    # straddle two rows (global path); zstage=0 forces the global path everywhere
+    a = gpu_synth(*spec, seed=8, coeff_mode="table")
+    b = gpu_synth(*spec, seed=8, coeff_mode="table")
+    p = gpu_synth(*spec, seed=8, coeff_mode="packed")
+    b.set_tuning("zstage", 0)
+    for _ in range(2):
+        for f in (a, b, p):
+            f.filter(1e-8)
+        for k in FIELDS:
+            assert np.array_equal(a.field(k), b.field(k)), k
+            assert np.array_equal(a.field(k), p.field(k)), k
+
+
 def test_gather_field_device_handoff():
     import torch
     f = gpu_synth(40, 33, 2, 6, seed=3)

@@ -284,9 +284,12 @@ def test_stage_api_matches_filter():
     assert a.rng_state() == b.rng_state()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_z_strips_in_process_match_single(world):
-    spec = dict(plane="synthetic", Ny=100, Nz=256, N_min=4, N_max=16, seed=8, device=0)
+@pytest.mark.parametrize("world,Nz,mode", [(2, 256, "packed"), (3, 256, "packed"), (2, 1100, "table"),
+                                            (3, 1700, "table")])
+def test_z_strips_in_process_match_single(world, Nz, mode):
+    # table cases: 4-5 strips per rank, so some blocks stage their row's noise (halo from
+    # the neighbour included) in LDS and others straddle rows
+    spec = dict(plane="synthetic", Ny=100, Nz=Nz, N_min=4, N_max=16, seed=8, device=0, coeff_mode=mode)
     whole = dfamd.DigitalFilter(**spec)
     strips = dfamd.create_group(world, **spec)
     for _ in range(2):

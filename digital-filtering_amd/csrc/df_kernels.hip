@@ -583,6 +583,17 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
             }
         }
     };
+    auto noise = [&](int t) { return DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t); };
+    auto body_n = [&](int t, const double2 n) {
+        double2 b[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) b[r] = coef(r, t);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc0[r] += b[r].x * n.x;
+            acc1[r] += b[r].y * n.y;
+        }
+    };
     auto body = [&](int t) {
         const double2 n = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t);
         double2 b[R];
@@ -601,6 +612,38 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     const int bh = body_ok ? Nlo : thi;
     int t = tlo;
     for (; t < bl; ++t) predicated(t);
+#if defined(DF_YPASS_NOPREFETCH)
+    constexpr bool kPrefetch = false; // timing-only variant
+#else
+    constexpr bool kPrefetch = true;
+#endif
+    if (kPrefetch && TABLE && !PC && YU < 4 && t + 1 <= bh) {
+        // VALU-bound table mode: the next two noise rows are in flight while this pair's
+        // taps run (the compiler would wait on each iteration's own loads)
+        // (two register pairs in ping-pong: no copies, so no wait at the end of an iteration)
+        double2 n0 = noise(t), n1 = noise(t + 1);
+        for (; t + 5 <= bh; t += 4) {
+            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            n0 = noise(t + 4);
+            n1 = noise(t + 5);
+            body_n(t + 2, m0);
+            body_n(t + 3, m1);
+        }
+        if (t + 3 <= bh) {
+            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            body_n(t + 2, m0);
+            body_n(t + 3, m1);
+            t += 4;
+        } else {
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            t += 2;
+        }
+    }
     if (YU >= 4) {
         for (; t + 3 <= bh; t += 4) {
             body(t);

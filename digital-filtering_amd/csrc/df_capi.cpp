@@ -90,6 +90,15 @@ struct df_handle {
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
     int zstage = 1;    // table z-pass noise staged in LDS
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
+    // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
+    // holds {y-pass -> z-pass} beside {K1 -> K2a -> K2b -> K2c -> K3 of the next call}, so a call
+    // is one hipGraphLaunch instead of ~10 API calls. Opt-in: measured SLOWER than the two-stream
+    // launches on ROCm 7 / MI355X (c1 43.8 -> 67.9 us per call, c2 table 48 -> 81 us;
+    // profiles/r1/probe/small_plane_latency.jsonl, same box), bit-identical either way.
+    int use_graph = 0;
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    double graph_dt[2] = {0, 0};
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
     CompDev c[3];
     double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr, *tabf = nullptr;
@@ -506,18 +515,19 @@ int build(df_handle *h, const df_config_c *cfg)
     h->rank = cfg->rank;
     h->world = cfg->world < 1 ? 1 : cfg->world;
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
-    // measured best on MI355X (tools/ab.py same-handle A/B, profiles/r1): packed 2, table 4
-    h->rows_per_wave = cfg->rows_per_wave > 0 ? cfg->rows_per_wave : (h->coeff_mode == DF_COEFF_TABLE ? 4 : 2);
+    h->rows_per_wave = cfg->rows_per_wave; // 0: chosen from the plane's shape after setup (below)
     // tuning knobs for in-process A/B experiments (tools/ab.py); defaults are the measured best
     if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_HEAVY_FIRST")) h->heavy_first = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YUNROLL")) h->yunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_ZUNROLL")) h->zunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_GRAPH")) h->use_graph = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
     if (h->solo_strip) h->split_count = true;
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
-    if (h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 && h->rows_per_wave != 8)
+    if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
+        h->rows_per_wave != 8)
         return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
 
     std::string err;
@@ -536,6 +546,21 @@ int build(df_handle *h, const df_config_c *cfg)
     for (int c = 0; c < 3; ++c)
         if (h->world > 1 && s.comp[c].Nz_max > h->Nz_loc)
             return fail(DF_EINVAL, "z-strip narrower than the z half-width: use fewer GPUs");
+    // Default launch shapes, measured on MI355X (tools/tune_sweep.py, tools/ab.py; profiles/r1/probe/
+    // tune_small_planes.jsonl): c3-class planes packed 2 rows per wave, table 4. Where a wave's serial tap chain
+    // rather than bandwidth sets the time - y half-widths >= 128 (the reference's own grid: 212) or
+    // under ~1 wave per SIMD - packed takes 1 row with the 8-deep load pipeline, table 2 rows.
+    if (h->rows_per_wave == 0) {
+        int nymax = 0;
+        for (int c = 0; c < 3; ++c) nymax = std::max(nymax, s.comp[c].Ny_max);
+        const bool long_chain = nymax >= 128;
+        const bool tiny = (long long)h->nstrips * ((s.Ny + 1) / 2) < 1024;
+        if (h->coeff_mode == DF_COEFF_TABLE) h->rows_per_wave = long_chain ? 2 : 4;
+        else if (long_chain || tiny) {
+            h->rows_per_wave = 1;
+            if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
+        } else h->rows_per_wave = 2;
+    }
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -595,6 +620,15 @@ int build(df_handle *h, const df_config_c *cfg)
         const double T = A / p * 1.002 + 16.0 * std::sqrt(A) + 8192.0;
         h->rng_blocks = (int)std::ceil(T / kRngBlockAttempts);
     }
+    // K3 splits each attempt wave over up to 16 waves while the plane has fewer than ~4 waves of
+    // attempts per SIMD (c1: 140 waves; the reference's grid: ~750): a wave's 16 serial polar
+    // iterations (log, sqrt, divide in FP64) otherwise set K3's time on small planes.
+    g.gen_split = 1;
+    while (g.gen_split < kRngPerThread && (long long)h->rng_blocks * kWavesPerBlock * g.gen_split < 4096)
+        g.gen_split *= 2;
+    if (const char *e = std::getenv("DFAMD_GEN_SPLIT")) g.gen_split = std::atoi(e);
+    if (g.gen_split < 1 || g.gen_split > kRngPerThread || (g.gen_split & (g.gen_split - 1)))
+        return fail(DF_EINVAL, "gen_split must be a power of two <= 16");
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -835,6 +869,10 @@ void destroy(df_handle *h)
     if (h->rng_comm) ncclCommDestroy(h->rng_comm);
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->ev_counted) (void)hipEventDestroy(h->ev_counted);
+    for (auto &g : h->graph)
+        if (g) (void)hipGraphExecDestroy(g);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     for (int set = 0; set < 2; ++set) {
         if (h->ev_rng[set]) (void)hipEventDestroy(h->ev_rng[set]);
         if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
@@ -846,6 +884,95 @@ void destroy(df_handle *h)
 
 // Strips of one plane held by handles of this process: each phase runs on every
 // handle before the halo copies, then the z-pass. corr_sra = false is step 0.
+void drop_graphs(df_handle *h)
+{
+    for (auto &g : h->graph)
+        if (g) {
+            (void)hipGraphExecDestroy(g);
+            g = nullptr;
+        }
+}
+
+// The graph path applies to the steady state of a single-GPU handle: next call's noise already
+// enqueued, no per-call events (profiling), no CSV, no RCCL.
+bool graph_ok(df_handle *h)
+{
+    return h->use_graph && h->overlap && h->world == 1 && !h->group && !h->profiling && h->csv_path.empty() &&
+           h->gen_launched == h->gen_used + 1;
+}
+
+// Capture one call for noise set `cur`: sweeps on stream, the next generation (into set cur^1,
+// state slot cur^1 -> cur) on rng_stream, forked from and joined back to stream.
+int capture_call(df_handle *h, int cur, double dt, hipGraphExec_t *out)
+{
+    if (!h->ev_fork) HIP_OR(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), DF_EHIP);
+    if (!h->ev_join) HIP_OR(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), DF_EHIP);
+    HIP_OR(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal), DF_EHIP);
+    int rc = DF_OK;
+    const int saved_cur = h->cur;
+    auto body = [&]() -> int {
+        HIP_OR(hipEventRecord(h->ev_fork, h->stream), DF_EHIP);
+        HIP_OR(hipStreamWaitEvent(h->rng_stream, h->ev_fork, 0), DF_EHIP);
+        h->cur = cur;
+        int r;
+        if ((r = phase_ypass(h, 7))) return r;
+        if ((r = phase_zpass(h, true, true, dt))) return r;
+        const int nxt = cur ^ 1;
+        RngGeom g = h->geom;
+        for (int c = 0; c < 3; ++c) {
+            g.ry[c] = h->c[c].ry[nxt];
+            g.rz[c] = h->c[c].rz[nxt];
+        }
+        HIP_OR(launch_rng_count(g, h->rstate + nxt, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks,
+                                h->rng_blocks, h->rng_stream),
+               DF_EHIP);
+        HIP_OR(launch_rng_finish(g, h->rstate + nxt, h->rstate + cur, h->counts, h->wave_counts, h->offsets,
+                                 h->part, h->masks, h->tasks, h->ntasks, h->err_dev, h->rng_blocks, h->rng_blocks,
+                                 h->rng_stream),
+               DF_EHIP);
+        HIP_OR(hipEventRecord(h->ev_join, h->rng_stream), DF_EHIP);
+        HIP_OR(hipStreamWaitEvent(h->stream, h->ev_join, 0), DF_EHIP);
+        return DF_OK;
+    };
+    rc = body();
+    h->cur = saved_cur;
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->stream, &graph); // always leave capture mode
+    if (rc) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc;
+    }
+    if (e != hipSuccess) return fail(DF_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+    const hipError_t ei = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) return fail(DF_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
+    return DF_OK;
+}
+
+// df_filter's steady state as one graph launch; bookkeeping mirrors consume_gen + prefetch_gen.
+int graph_call(df_handle *h, double dt)
+{
+    if (h->gen_used > 0) HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP);
+    const int cur = (int)(h->gen_used & 1);
+    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[cur], 0), DF_EHIP); // this call's noise (maybe non-graph)
+    hipGraphExec_t &g = h->graph[cur];
+    if (g && h->graph_dt[cur] != dt) {
+        (void)hipGraphExecDestroy(g);
+        g = nullptr;
+    }
+    if (!g) {
+        int rc = capture_call(h, cur, dt, &g);
+        if (rc) return rc;
+        h->graph_dt[cur] = dt;
+    }
+    h->cur = cur;
+    h->gen_used++;
+    HIP_OR(hipGraphLaunch(g, h->stream), DF_EHIP);
+    HIP_OR(hipEventRecord(h->ev_rng[cur ^ 1], h->stream), DF_EHIP); // next call's noise is ready with the graph
+    h->gen_launched++;
+    return DF_OK;
+}
+
 int group_step(df_handle **hs, int n, bool corr_sra, double dt)
 {
     if (!hs || n < 1) return fail(DF_EINVAL, "empty handle group");
@@ -961,6 +1088,7 @@ int df_filter(df_handle *h, double dt)
     if (h->world > 1 && !h->comm && !h->solo_strip)
         return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    if (graph_ok(h)) return graph_call(h, dt);
     const bool prof = prof_on(h);
     if ((rc = consume_gen(h))) return rc;
     ev_record(h, 0);
@@ -1242,12 +1370,19 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->rows_per_wave = value;
     } else if (k == "nt_loads") h->nt_loads = value != 0;
     else if (k == "heavy_first") h->heavy_first = value != 0;
-    else if (k == "yunroll") h->yunroll = value >= 4 ? 4 : 2;
+    else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
+    else if (k == "graph") h->use_graph = value != 0;
+    else if (k == "gen_split") {
+        if (value < 1 || value > kRngPerThread || (value & (value - 1)))
+            return fail(DF_EINVAL, "gen_split must be 1, 2, 4, 8 or 16");
+        h->geom.gen_split = value;
+    }
     else return fail(DF_EINVAL, "unknown tuning key: " + k);
+    drop_graphs(h); // captured launches carry the old shapes
     return DF_OK;
 }
 

@@ -362,7 +362,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
                                                                   const uint16_t *__restrict__ masks)
 {
     const int lane = threadIdx.x & 63;
-    const int slot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    const int split = g.gen_split; // power of two <= kRngPerThread
+    const int vslot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    const int slot = vslot / split, sub = vslot - slot * split;
     if (slot >= *ntasks) return;
     const int gw = uniform(tasks[slot].gw);
     long long rank_w = tasks[slot].r_lo; // uniform
@@ -371,10 +373,17 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
     uint64_t st = thread_first_state(g, sin->state, b, tid); // start of attempt m
+    // This wave runs iterations [m0, m1) of the attempt wave: the state jumps over the first m0
+    // attempts of the lane and the rank over the whole wave's accepts among them.
+    const int per = kRngPerThread / split, m0 = sub * per, m1 = m0 + per;
+    for (int m = 0; m < m0; ++m) {
+        st = g.next_mult * st + g.next_plus;
+        rank_w += __popcll(__ballot((bits >> m) & 1u));
+    }
     // The wave's runs of iterations m, m+1, ... are consecutive in the stream (wave-major ranks),
     // so its position is located once and then advanced by 2*n_acc per iteration.
     StreamPos P = stream_pos(g, f + 2ull * (uint64_t)rank_w);
-    for (int m = 0; m < kRngPerThread; ++m) {
+    for (int m = m0; m < m1; ++m) {
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
         // The wave's accepted attempts own the contiguous positions
@@ -493,8 +502,8 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
     const int nw = nb_total * (kRngThreads / 64);
     hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part, wave_counts,
                        nb_total, tasks, ntasks);
-    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, st_out, tasks, ntasks,
-                       masks);
+    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in, st_out,
+                       tasks, ntasks, masks);
     return hipGetLastError();
 }
 
@@ -528,6 +537,9 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     const int nr = min(R, Ny - j0);
     const int col = s * kStrip + 2 * lane;
     const int Pz = a.Pz;
+    // Lanes wholly in the last strip's padding leave: every later load then fetches only the
+    // live lanes' bytes (Nz = 400 on the reference's grid: 22% of a 512-wide stream)
+    if (col >= a.Nz_loc) return;
 
     int N[R];
     const double *bp[R];
@@ -617,6 +629,38 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 #else
     constexpr bool kPrefetch = true;
 #endif
+    if (YU >= 8 && !PC && t + YU - 1 <= bh) {
+        // Deep pipeline (yunroll 8): a ring of YU taps' noise and coefficients in registers;
+        // slot u is refilled with tap t+u+YU right after it is consumed, so YU taps are always
+        // in flight. For planes with few waves per SIMD and wide stencils (the reference's own
+        // grid: N_y up to 212) a wave's serial load->use chain, not HBM bandwidth, sets the time.
+        double2 nb[YU], cb[YU][R];
+#pragma unroll
+        for (int u = 0; u < YU; ++u) {
+            nb[u] = noise(t + u);
+#pragma unroll
+            for (int r = 0; r < R; ++r) cb[u][r] = coef(r, t + u);
+        }
+        auto use = [&](const double2 n, const double2 *b) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                acc0[r] += b[r].x * n.x;
+                acc1[r] += b[r].y * n.y;
+            }
+        };
+        for (; t + 2 * YU - 1 <= bh; t += YU) {
+#pragma unroll
+            for (int u = 0; u < YU; ++u) {
+                use(nb[u], cb[u]);
+                nb[u] = noise(t + u + YU);
+#pragma unroll
+                for (int r = 0; r < R; ++r) cb[u][r] = coef(r, t + u + YU);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
+        t += YU;
+    }
     if (kPrefetch && TABLE && !PC && YU < 4 && t + 1 <= bh) {
         // VALU-bound table mode: the next two noise rows are in flight while this pair's
         // taps run (the compiler would wait on each iteration's own loads)
@@ -688,12 +732,16 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     if (TABLE && a.per_cell)
         hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
     else if (!TABLE && a.nt_loads) {
-        if (a.yunroll >= 4)
+        if (a.yunroll >= 8)
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
+        else if (a.yunroll >= 4)
             hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
         else
             hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
     } else {
-        if (a.yunroll >= 4)
+        if (a.yunroll >= 8)
+            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
+        else if (a.yunroll >= 4)
             hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
         else
             hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
@@ -758,6 +806,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             __syncthreads();
         }
     }
+    if (col >= a.Nz_loc) return; // padding lanes (after their share of the staging copy)
 
     double f0[3], f1[3];
 #pragma unroll

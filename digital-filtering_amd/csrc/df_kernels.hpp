@@ -57,6 +57,8 @@ struct RngGeom {
     uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
     int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw
     int nt_stores;                 // noise pairs stored non-temporally
+    int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
+                                   // iterations, so few-wave planes get short serial chains
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];

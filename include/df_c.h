@@ -75,7 +75,7 @@ typedef struct df_config_c {
                                               queries only, no GPU: used by CPU tests) */
     int rank, world;                       /* z-strip partition: this GPU is strip `rank` of `world` */
     const void *comm_id;                   /* 128-byte RCCL unique id (world > 1), from df_comm_unique_id */
-    int rows_per_wave;                     /* y-pass register blocking (tuning knob, 0 = default) */
+    int rows_per_wave;                     /* y-pass register blocking (tuning knob, 0 = from the plane's shape) */
     int rng_resume;                        /* 1: start the stream at (rng_state, rng_saved_flag, rng_saved) */
     int rng_saved_flag;                    /*    instead of seeding (checkpoint/resume, and continuing */
     uint64_t rng_state;                    /*    the reference's process-wide stream across instances) */
@@ -184,7 +184,10 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
                     const long long *dst_cell, long long dst_len, double beta);
 
 /* Launch-shape tuning (extension; results are bit-identical for every setting):
- * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4), "zunroll" (2,4), "nt_stores", "rng_nt_stores". */
+ * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4; 8 = 8-deep load pipeline),
+ * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS),
+ * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "graph" (steady-state
+ * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* Timing (hipEvents on the handle's stream). */

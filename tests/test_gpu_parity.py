@@ -131,9 +131,14 @@ def test_golden_synthetic(name):
     check_golden_case(name)
 
 
-def test_golden_native_grid():
+@pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8)),
+                                         ("table", dict(yunroll=8))])
+def test_golden_native_grid(mode, tuning):
+    # the reference's own grid (N_y up to 212): default shapes and the deep y-pass pipeline
     g = np.load(os.path.join(GOLDEN, "native_s42.npz"))
-    f = dfamd.DigitalFilter(seed=42, device=0)
+    f = dfamd.DigitalFilter(seed=42, device=0, coeff_mode=mode)
+    for k, v in tuning.items():
+        f.set_tuning(k, v)
     assert (f.Ny, f.Nz) == (510, 400)
     rows = list(g["sample_rows"])
     for s in range(int(g["nsteps"]) + 1):
@@ -208,7 +213,9 @@ def test_runtime_tuning_is_bitexact(mode):
     b = gpu_synth(*spec, seed=5, coeff_mode=mode)
     settings = [dict(rows_per_wave=1, zunroll=4, yunroll=4), dict(rows_per_wave=8, nt_loads=0, heavy_first=0),
                 dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_loads=1, heavy_first=1, nt_stores=1),
-                dict(nt_stores=0)]
+                dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8), dict(rows_per_wave=4, yunroll=8, nt_loads=0),
+                dict(rows_per_wave=2, yunroll=8, nt_loads=1), dict(gen_split=1), dict(gen_split=4),
+                dict(gen_split=16)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -216,6 +223,7 @@ def test_runtime_tuning_is_bitexact(mode):
         b.filter(1e-8)
         for k in FIELDS:
             assert np.array_equal(a.field(k), b.field(k)), (kw, k)
+        assert a.rng_state() == b.rng_state(), kw
     with pytest.raises(dfamd.DFError, match="unknown tuning"):
         b.set_tuning("warp_size", 32)
     with pytest.raises(dfamd.DFError, match="rows_per_wave"):
@@ -236,6 +244,38 @@ def test_table_lds_staging_is_bitexact(spec):
         for k in FIELDS:
             assert np.array_equal(a.field(k), b.field(k)), k
             assert np.array_equal(a.field(k), p.field(k)), k
+
+
+@pytest.mark.parametrize("mode", ["packed", "table"])
+def test_graph_path_matches_stream_path(mode):
+    # filter() replays a captured HIP graph in the steady state; switching to the stream path
+    # (profiling on, graph off) and back, changing dt (re-capture) and moving the RNG state must
+    # leave fields and stream state bit-identical to a handle that never uses graphs
+    spec = (96, 300, 2, 12)
+    g = gpu_synth(*spec, seed=21, coeff_mode=mode)
+    s = gpu_synth(*spec, seed=21, coeff_mode=mode)
+    g.set_tuning("graph", 1)
+    s.set_tuning("graph", 0)
+    plan = [("dt", 1e-8), ("dt", 1e-8), ("dt", 2e-8), ("prof", 1e-8), ("dt", 1e-8), ("off", 1e-8), ("on", 1e-5),
+            ("state", 1e-8), ("dt", 1e-8)]
+    other = gpu_synth(*spec, seed=99, coeff_mode=mode).rng_state()
+    for what, dt in plan:
+        if what == "prof":
+            g.set_profiling(True)
+        elif what == "off":
+            g.set_profiling(False)
+            g.set_tuning("graph", 0)
+        elif what == "on":
+            g.set_tuning("graph", 1)
+        elif what == "state":
+            g.set_rng_state(*other)
+            s.set_rng_state(*other)
+        g.filter(dt)
+        s.filter(dt)
+        for k in FIELDS:
+            assert np.array_equal(g.field(k), s.field(k)), (what, k)
+        assert g.rng_state() == s.rng_state(), what
+    g.set_profiling(False)
 
 
 def test_gather_field_device_handoff():

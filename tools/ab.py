@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
 import dfamd  # noqa: E402
 
-CFG = {"c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64)}
+CFG = {"c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64),
+       "native": None}  # the reference's own grid and profiles (510 x 400)
 
 
 def make(envspec, cfg, mode, rpw):
@@ -32,9 +33,12 @@ def make(envspec, cfg, mode, rpw):
         k, v = kv.split("=")
         saved[k] = os.environ.get(k)
         os.environ[k] = v
-    Ny, Nz, a, b = CFG[cfg]
-    f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=a, N_max=b, seed=1, device=0,
-                            coeff_mode=mode, rows_per_wave=rpw)
+    if CFG[cfg] is None:
+        f = dfamd.DigitalFilter(plane=cfg, seed=1, device=0, coeff_mode=mode, rows_per_wave=rpw)
+    else:
+        Ny, Nz, a, b = CFG[cfg]
+        f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=a, N_max=b, seed=1, device=0,
+                                coeff_mode=mode, rows_per_wave=rpw)
     for k, v in saved.items():
         if v is None:
             os.environ.pop(k)

@@ -88,6 +88,7 @@ struct df_handle {
     int heavy_first = 1;
     int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
+    int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
@@ -202,6 +203,10 @@ SweepArgs sweep_args(df_handle *h)
     a.yunroll = h->yunroll;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
+    a.ywin_T = h->ywin_T;
+    a.ywin_W = h->ywin_W;
+    a.zwin_T = h->zwin_T;
+    a.zwin_W = h->zwin_W;
     a.per_cell = h->setup.per_cell;
     int nzp = 0;
     for (int c = 0; c < 3; ++c) nzp = std::max(nzp, a.Nzp[c]);
@@ -831,13 +836,15 @@ int build(df_handle *h, const df_config_c *cfg)
         if ((rc = dalloc_t(h, &h->send_r, h->halo_elems))) return rc;
         if ((rc = dalloc_t(h, &h->recv_l, h->halo_elems))) return rc;
         if ((rc = dalloc_t(h, &h->recv_r, h->halo_elems))) return rc;
-        if (cfg->comm_id) {
-            ncclUniqueId id;
-            std::memcpy(&id, cfg->comm_id, sizeof(id));
-            NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
-            NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
-            h->split_count = true;
-        }
+    }
+    // A communicator of one rank is accepted too: the same init, split and grouped all-gather then run on a
+    // single GPU (tests/test_gpu_parity.py::test_rccl_single_rank_matches_plain), the halo being a no-op.
+    if (cfg->comm_id) {
+        ncclUniqueId id;
+        std::memcpy(&id, cfg->comm_id, sizeof(id));
+        NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
+        NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
+        h->split_count = true;
     }
     for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
@@ -1376,6 +1383,14 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "graph") h->use_graph = value != 0;
+    else if (k == "ywin_T" || k == "zwin_T") {
+        if (value < 0 || value > (1 << 24) || (value & (value - 1)))
+            return fail(DF_EINVAL, k + " must be 0 or a power of two <= 2^24 (ticks of the 100 MHz clock)");
+        (k[0] == 'y' ? h->ywin_T : h->zwin_T) = value;
+    } else if (k == "ywin_W" || k == "zwin_W") {
+        if (value < 0) return fail(DF_EINVAL, k + " must be >= 0");
+        (k[0] == 'y' ? h->ywin_W : h->zwin_W) = value;
+    }
     else if (k == "gen_split") {
         if (value < 1 || value > kRngPerThread || (value & (value - 1)))
             return fail(DF_EINVAL, "gen_split must be 1, 2, 4, 8 or 16");

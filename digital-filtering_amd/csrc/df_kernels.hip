@@ -507,6 +507,15 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
     return hipGetLastError();
 }
 
+
+// Hold this wave's output stores until the next write window (SweepArgs::ywin_T/zwin_T).
+__device__ __forceinline__ void write_window(int T, int W)
+{
+    if (T <= 0) return;
+    const uint64_t m = (uint64_t)T - 1;
+    while ((__builtin_amdgcn_s_memrealtime() & m) >= (uint64_t)W) __builtin_amdgcn_s_sleep(8);
+}
+
 // ---------------------------------------------------------------- K4 y-pass
 //
 // One wave = one tile of R consecutive rows x one 128-cell strip; lane l owns
@@ -703,6 +712,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     for (; t <= bh; ++t) body(t);
     for (; t <= thi; ++t) predicated(t);
 
+    write_window(a.ywin_T, a.ywin_W);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < nr) {
@@ -944,6 +954,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
     double fu[2] = {f0[0], f1[0]}, fv[2] = {f0[1], f1[1]}, fw[2] = {f0[2], f1[2]};
     if (a.do_corr) { // df.cpp:415
         const double2 ou = ld(a.filt_old[0]), ov = ld(a.filt_old[1]), ow = ld(a.filt_old[2]);
+        write_window(a.zwin_T, a.zwin_W); // the filt_old loads are in flight meanwhile
         const double o[3][2] = {{ou.x, ou.y}, {ov.x, ov.y}, {ow.x, ow.y}};
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -952,6 +963,8 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             fw[e] = o[2][e] * a.sa[2] + fw[e] * a.s1a[2];
         }
     }
+    else
+        write_window(a.zwin_T, a.zwin_W);
     double up[2], vp[2], wp[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {

@@ -74,7 +74,8 @@ typedef struct df_config_c {
     int device;                            /* HIP device ordinal; -1 = host-only handle (setup
                                               queries only, no GPU: used by CPU tests) */
     int rank, world;                       /* z-strip partition: this GPU is strip `rank` of `world` */
-    const void *comm_id;                   /* 128-byte RCCL unique id (world > 1), from df_comm_unique_id */
+    const void *comm_id;                   /* 128-byte RCCL unique id, from df_comm_unique_id (world > 1;
+                                              world 1 also accepted: exercises the same RCCL calls) */
     int rows_per_wave;                     /* y-pass register blocking (tuning knob, 0 = from the plane's shape) */
     int rng_resume;                        /* 1: start the stream at (rng_state, rng_saved_flag, rng_saved) */
     int rng_saved_flag;                    /*    instead of seeding (checkpoint/resume, and continuing */

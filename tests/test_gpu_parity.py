@@ -341,6 +341,23 @@ def test_z_strips_in_process_match_single(world, Nz, mode):
     assert all(s.rng_state() == whole.rng_state() for s in strips)
 
 
+def test_rccl_single_rank_matches_plain():
+    # The RCCL calls of the z-strip path (ncclCommInitRank, ncclCommSplit, the grouped in-place
+    # ncclAllGather of block counts, wave counts and accept masks on the RNG stream) run here with a
+    # communicator of one rank; results must equal the plain single-GPU handle bit for bit.
+    spec = dict(plane="synthetic", Ny=96, Nz=300, N_min=4, N_max=16, seed=5, device=0)
+    plain = dfamd.DigitalFilter(**spec)
+    rc = dfamd.DigitalFilter(rank=0, world=1, comm_id=dfamd.comm_unique_id(), **spec)
+    for dt in (1e-8, 1e-8, 1e-5):
+        plain.filter(dt)
+        rc.filter(dt)
+        for k in FIELDS:
+            assert np.array_equal(rc.field(k), plain.field(k)), k
+        assert rc.rng_state() == plain.rng_state()
+    rc.close()
+    plain.close()
+
+
 def test_set_rng_state_discards_prefetched_noise():
     # The next call's noise is generated ahead of time on a second stream; moving the
     # stream must regenerate it (df.cpp:334-335 semantics: draws follow the state).

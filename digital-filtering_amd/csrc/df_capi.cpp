@@ -587,6 +587,22 @@ int build(df_handle *h, const df_config_c *cfg)
         }
     }
 
+    // Write windows (SweepArgs::ywin_T): on planes whose sweeps stream >= 2 GB of packed coefficients per
+    // pass the waves hold their stores for a chip-wide window of 2.56 us every 41 us; c3 -5.1% per call,
+    // c5 -3.1% (profiles/r1/probe/win_*.json). Smaller planes (c2: +4.7%) and the VALU-bound table mode
+    // (+40%) store at once.
+    {
+        long long by = 0, bz = 0;
+        for (int c = 0; c < 3; ++c) {
+            by += h->c[c].by_size;
+            bz += h->c[c].bz_size;
+        }
+        if (h->coeff_mode != DF_COEFF_TABLE && !std::getenv("DFAMD_NO_WRITE_WINDOWS")) {
+            if (8 * by >= 2000000000LL) h->ywin_T = 4096, h->ywin_W = 256;
+            if (8 * bz >= 2000000000LL) h->zwin_T = 4096, h->zwin_W = 256;
+        }
+    }
+
     // ---- RNG stream geometry (df.cpp:343-348 order) and launch size
     RngGeom &g = h->geom;
     g.seg[0] = 0;

@@ -511,7 +511,7 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 // Hold this wave's output stores until the next write window (SweepArgs::ywin_T/zwin_T).
 __device__ __forceinline__ void write_window(int T, int W)
 {
-    if (T <= 0) return;
+    if (T <= 0 || W <= 0) return; // W = 0 would never open: treated as off
     const uint64_t m = (uint64_t)T - 1;
     while ((__builtin_amdgcn_s_memrealtime() & m) >= (uint64_t)W) __builtin_amdgcn_s_sleep(8);
 }

@@ -95,7 +95,7 @@ struct SweepArgs {
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is
     // in the first W ticks of a T-tick period, so the CUs write together and the read stream runs
-    // write-free in between (tools/write_probe). T a power of two; 0 = store at once. Per pass.
+    // write-free in between (tools/write_probe). T a power of two; T or W = 0: store at once. Per pass.
     int ywin_T, ywin_W, zwin_T, zwin_W;
 };
 

@@ -215,7 +215,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_loads=1, heavy_first=1, nt_stores=1),
                 dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8), dict(rows_per_wave=4, yunroll=8, nt_loads=0),
                 dict(rows_per_wave=2, yunroll=8, nt_loads=1), dict(gen_split=1), dict(gen_split=4),
-                dict(gen_split=16)]
+                dict(gen_split=16), dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256),
+                dict(ywin_T=0, zwin_T=4096, zwin_W=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -228,6 +229,8 @@ def test_runtime_tuning_is_bitexact(mode):
         b.set_tuning("warp_size", 32)
     with pytest.raises(dfamd.DFError, match="rows_per_wave"):
         b.set_tuning("rows_per_wave", 3)
+    with pytest.raises(dfamd.DFError, match="power of two"):
+        b.set_tuning("zwin_T", 3000)
 
 
 @pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90)])

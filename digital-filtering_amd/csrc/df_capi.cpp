@@ -88,6 +88,7 @@ struct df_handle {
     int heavy_first = 1;
     int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
+    int ynt_stores = 1; // the y-pass output likewise
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
@@ -203,6 +204,7 @@ SweepArgs sweep_args(df_handle *h)
     a.yunroll = h->yunroll;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
+    a.ynt_stores = h->ynt_stores;
     a.ywin_T = h->ywin_T;
     a.ywin_W = h->ywin_W;
     a.zwin_T = h->zwin_T;
@@ -1395,7 +1397,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "heavy_first") h->heavy_first = value != 0;
     else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
-    else if (k == "nt_stores") h->nt_stores = value != 0;
+    else if (k == "nt_stores") h->nt_stores = h->ynt_stores = value != 0;
+    else if (k == "znt_stores") h->nt_stores = value != 0;
+    else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "graph") h->use_graph = value != 0;

@@ -513,7 +513,14 @@ __device__ __forceinline__ void write_window(int T, int W)
 {
     if (T <= 0 || W <= 0) return; // W = 0 would never open: treated as off
     const uint64_t m = (uint64_t)T - 1;
-    while ((__builtin_amdgcn_s_memrealtime() & m) >= (uint64_t)W) __builtin_amdgcn_s_sleep(8);
+    // bounded: a wave waits at most ~T ticks of the clock, and never more than 8192 sleeps (~1.7 ms)
+    // whatever the counter does, so every wave reaches its stores and the grid drains
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < 8192; ++it) {
+        const uint64_t t = __builtin_amdgcn_s_memrealtime();
+        if ((t & m) < (uint64_t)W || t - t0 > (uint64_t)T) break;
+        __builtin_amdgcn_s_sleep(8);
+    }
 }
 
 // ---------------------------------------------------------------- K4 y-pass
@@ -725,7 +732,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
             if (acc0[r] != 1234.5) continue; // timing only
 #endif
             if (col + 1 < a.Nz_loc) {
-                if (a.nt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
+                if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
                 else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
             }
             else if (col < a.Nz_loc) o[0] = acc0[r];

@@ -90,7 +90,8 @@ struct SweepArgs {
     int nt_loads;           // non-temporal loads for the coefficient stream
     int heavy_first;        // schedule rows with the widest stencils first
     int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
-    int nt_stores;          // sweep outputs stored non-temporally
+    int nt_stores;          // z-pass outputs stored non-temporally
+    int ynt_stores;         // y-pass output (r_zs) stored non-temporally
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is

@@ -146,6 +146,29 @@ __global__ __launch_bounds__(256) void wait_kernel(const dvec2 *__restrict__ p, 
     for (int w = 0; w < Wk; ++w) __builtin_nontemporal_store(acc, o + (size_t)w * 64);
 }
 
+// wait_kernel plus reads paused inside the windows: a wave about to issue a group of loads while
+// the window is open sleeps until it closes, so windows carry (almost) only writes
+__global__ __launch_bounds__(256) void pause_kernel(const dvec2 *__restrict__ p, dvec2 *__restrict__ out,
+                                                    int nchunks, int S, int Wk, unsigned T, unsigned W)
+{
+    const int lane = threadIdx.x & 63;
+    const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (c >= nchunks) return;
+    const dvec2 *q = p + (size_t)c * S * 64 + lane;
+    dvec2 acc = {0, 0};
+    for (int s = 0; s + 4 <= S; s += 4) {
+        while ((unsigned)(__builtin_amdgcn_s_memrealtime() & (T - 1)) < W) __builtin_amdgcn_s_sleep(4);
+        dvec2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(q + (size_t)(s + u) * 64);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    while ((unsigned)(__builtin_amdgcn_s_memrealtime() & (T - 1)) >= W) __builtin_amdgcn_s_sleep(16);
+    dvec2 *o = out + (size_t)c * Wk * 64 + lane;
+    for (int w = 0; w < Wk; ++w) __builtin_nontemporal_store(acc, o + (size_t)w * 64);
+}
+
 int main(int argc, char **argv)
 {
     const size_t gib = argc > 1 ? strtoull(argv[1], 0, 10) : 8;
@@ -205,8 +228,14 @@ int main(int argc, char **argv)
         hipLaunchKernelGGL(wk_kernel, dim3(blocks1), dim3(256), 0, 0, a, wout, nchunks, S, Wk, 3, 1, sink);
         hipLaunchKernelGGL(wk_kernel, dim3(blocks1), dim3(256), 0, 0, a, wout, nchunks, 0, Wk, 1, 1, sink);
     }));
-    for (unsigned T : {1024u, 4096u, 16384u})
-        for (unsigned W : {T / 16, T / 8}) {
+    for (unsigned T : {2048u, 4096u})
+        for (unsigned W : {32u, 64u, 128u}) {
+            printf(", \"pause_T%u_W%u\": %.1f", T, W, timeit([&] {
+                hipLaunchKernelGGL(pause_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, 0, a, wout, nchunks, S, Wk, T, W);
+            }));
+        }
+    for (unsigned T : {2048u, 4096u, 8192u})
+        for (unsigned W : {32u, 64u, 128u, 256u, 512u}) {
             printf(", \"wait_T%u_W%u\": %.1f", T, W, timeit([&] {
                 hipLaunchKernelGGL(wait_kernel, dim3((nchunks + 3) / 4), dim3(256), 0, 0, a, wout, nchunks, S, Wk, T, W);
             }));

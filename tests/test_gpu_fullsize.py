@@ -143,6 +143,42 @@ def test_c3_z_strips_in_process_match_single():
     assert all(s.rng_state() == whole.rng_state() for s in strips)
 
 
+def test_c4_eight_z_strips_sampled_rows():
+    """c4 (BASELINE configs[3]: 2048 x 8192, 8 z-strips of 1024 columns): the eight strips of
+    the multi-GPU partition, run in one process (device-to-device halo and count copies in
+    place of the RCCL calls), against the sampled-row restatement of the whole plane. Each
+    strip's stream state must equal the single-stream state after every call."""
+    spec = dict(Ny=2048, Nz=8192, N_min=4, N_max=64)
+    seed = 404
+    strips = dfamd.create_group(8, plane="synthetic", seed=seed, device=0, **spec)
+    assert [s.Nz_loc for s in strips] == [1024] * 8
+    m = RowModel(spec, seed)
+    rows = [0, 409, 410, 2047]
+    for dt in (None, 1e-8):
+        if dt is not None:
+            dfamd.filter_group(strips, dt)
+        ref = m.step(rows, dt)
+        assert all(s.rng_state() == m.rng.state for s in strips)
+        for k in ("u", "v", "w", "T", "rho"):
+            cat = np.concatenate([s.field(k)[rows] for s in strips], axis=1)
+            assert float(rel_err(cat, ref[k]).max()) <= 1e-6, (dt, k)
+    for s in strips:
+        s.close()
+
+
+def test_c4_eight_z_strips_table_match_single():
+    spec = dict(plane="synthetic", seed=405, device=0, coeff_mode="table", Ny=2048, Nz=8192, N_min=4, N_max=64)
+    whole = dfamd.DigitalFilter(**spec)
+    strips = dfamd.create_group(8, **spec)
+    for _ in range(2):
+        whole.filter(1e-8)
+        dfamd.filter_group(strips, 1e-8)
+    for k in ("u", "v", "w", "T", "rho"):
+        cat = np.concatenate([s.field(k) for s in strips], axis=1)
+        assert np.array_equal(cat, whole.field(k)), k
+    assert all(s.rng_state() == whole.rng_state() for s in strips)
+
+
 def test_c5_full_size_sampled_rows():
     """c5 (4096 x 4096, N 4-64): 85 GB of offset-packed coefficients on one GPU; the
     Sigma(2N+1) = 1.7e9 offsets exceed nothing (64-bit on the device)."""

@@ -91,6 +91,8 @@ struct df_handle {
     int ynt_stores = 1; // the y-pass output likewise
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
+    int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
+    int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
     // holds {y-pass -> z-pass} beside {K1 -> K2a -> K2b -> K2c -> K3 of the next call}, so a call
@@ -114,7 +116,7 @@ struct df_handle {
     int *wave_counts = nullptr; // accepted attempts per wave of each block (K1 -> K2c)
     WaveTask *tasks = nullptr;  // waves K3 runs (K2c)
     int *ntasks = nullptr;
-    int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped
+    int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped, [2] halo loopback mismatches
     int *err_host = nullptr;
     int rng_blocks = 0;       // attempt blocks per call (4096 attempts each), same on every rank
     int rng_chunk = 0;        // blocks counted by each z-strip rank (split counting, SURVEY 8e option A)
@@ -202,6 +204,7 @@ SweepArgs sweep_args(df_handle *h)
     a.nt_loads = h->nt_loads;
     a.heavy_first = h->heavy_first;
     a.yunroll = h->yunroll;
+    a.ywindow = h->ywindow;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
     a.ynt_stores = h->ynt_stores;
@@ -217,10 +220,26 @@ SweepArgs sweep_args(df_handle *h)
     return a;
 }
 
+int alloc_halo(df_handle *h)
+{
+    h->halo_elems = 0;
+    for (int c = 0; c < 3; ++c) h->halo_elems += (size_t)h->Ny * h->c[c].Nzp;
+    int rc;
+    if ((rc = dalloc_t(h, &h->send_l, h->halo_elems))) return rc;
+    if ((rc = dalloc_t(h, &h->send_r, h->halo_elems))) return rc;
+    if ((rc = dalloc_t(h, &h->recv_l, h->halo_elems))) return rc;
+    return dalloc_t(h, &h->recv_r, h->halo_elems);
+}
+
 int check_rng_error(df_handle *h)
 {
     if (h->err_host && *(volatile int *)h->err_host)
         return fail(DF_ERNG, "device RNG ran short of polar attempts; stream state is invalid");
+    if (h->err_host && ((volatile int *)h->err_host)[2]) {
+        const int bad = ((volatile int *)h->err_host)[2];
+        h->err_host[2] = 0;
+        return fail(DF_ECOMM, "RCCL halo loopback: " + std::to_string(bad) + " values arrived changed");
+    }
     return DF_OK;
 }
 
@@ -430,9 +449,29 @@ int phase_halo_unpack(df_handle *h)
     return DF_OK;
 }
 
+// One-rank communicator with halo_loopback set: the grouped ncclSend/ncclRecv of the z-strip path
+// run with this rank as its own left and right neighbour (both plane edges packed, sent, received
+// and compared on the device); the received columns are not unpacked, so results are unchanged.
+int halo_loopback(df_handle *h)
+{
+    SweepArgs a = sweep_args(h);
+    HIP_OR(launch_halo_pack(a, h->send_l, h->send_r, h->stream), DF_EHIP);
+    NCCL_OR(ncclGroupStart());
+    NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, 0, h->comm, h->stream));
+    NCCL_OR(ncclRecv(h->recv_l, h->halo_elems, ncclDouble, 0, h->comm, h->stream));
+    NCCL_OR(ncclSend(h->send_r, h->halo_elems, ncclDouble, 0, h->comm, h->stream));
+    NCCL_OR(ncclRecv(h->recv_r, h->halo_elems, ncclDouble, 0, h->comm, h->stream));
+    NCCL_OR(ncclGroupEnd());
+    HIP_OR(launch_halo_check(h->send_l, h->recv_l, h->halo_elems, h->halo_loopback == 2, h->err_dev + 2, h->stream),
+           DF_EHIP);
+    HIP_OR(launch_halo_check(h->send_r, h->recv_r, h->halo_elems, 0, h->err_dev + 2, h->stream), DF_EHIP);
+    return DF_OK;
+}
+
 int phase_halo_rccl(df_handle *h)
 {
-    if (h->world == 1 || h->solo_strip) return DF_OK;
+    if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
+    if (h->solo_strip) return DF_OK;
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
     int rc = phase_halo_pack(h);
     if (rc) return rc;
@@ -702,7 +741,7 @@ int build(df_handle *h, const df_config_c *cfg)
         const int n = kv.first;
         for (int i = -n; i <= n; ++i) tabf_h.push_back(kv.second[i < 0 ? -i : i]);
     }
-    tabf_h.resize(tabf_h.size() + 8, 0.0);
+    tabf_h.resize(tabf_h.size() + 16, 0.0); // slack for the sweeps' whole-window scalar loads
     int rc;
     if ((rc = dalloc_t(h, &h->tab, tab_h.size()))) return rc;
     if ((rc = dalloc_t(h, &h->tab_off, tab_off_h.size()))) return rc;
@@ -836,8 +875,8 @@ int build(df_handle *h, const df_config_c *cfg)
         h->geom.jump_block = djb;
         h->geom.jump_thread = djt;
     }
-    HIP_OR(hipHostMalloc((void **)&h->err_host, 2 * sizeof(int), hipHostMallocMapped), DF_EHIP);
-    h->err_host[0] = h->err_host[1] = 0;
+    HIP_OR(hipHostMalloc((void **)&h->err_host, 3 * sizeof(int), hipHostMallocMapped), DF_EHIP);
+    h->err_host[0] = h->err_host[1] = h->err_host[2] = 0;
     HIP_OR(hipHostGetDevicePointer((void **)&h->err_dev, h->err_host, 0), DF_EHIP);
 
     uint64_t seed = cfg->seed;
@@ -847,14 +886,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = upload(h, h->rstate, &st0, 1))) return rc;
 
     // ---- halo buffers + communicator
-    if (h->world > 1) {
-        h->halo_elems = 0;
-        for (int c = 0; c < 3; ++c) h->halo_elems += (size_t)Ny * h->c[c].Nzp;
-        if ((rc = dalloc_t(h, &h->send_l, h->halo_elems))) return rc;
-        if ((rc = dalloc_t(h, &h->send_r, h->halo_elems))) return rc;
-        if ((rc = dalloc_t(h, &h->recv_l, h->halo_elems))) return rc;
-        if ((rc = dalloc_t(h, &h->recv_r, h->halo_elems))) return rc;
-    }
+    if (h->world > 1 && (rc = alloc_halo(h))) return rc;
     // A communicator of one rank is accepted too: the same init, split and grouped all-gather then run on a
     // single GPU (tests/test_gpu_parity.py::test_rccl_single_rank_matches_plain), the halo being a no-op.
     if (cfg->comm_id) {
@@ -922,7 +954,8 @@ void drop_graphs(df_handle *h)
 // enqueued, no per-call events (profiling), no CSV, no RCCL.
 bool graph_ok(df_handle *h)
 {
-    return h->use_graph && h->overlap && h->world == 1 && !h->group && !h->profiling && h->csv_path.empty() &&
+    return h->use_graph && h->overlap && h->world == 1 && !h->group && !h->profiling && !h->halo_loopback &&
+           h->csv_path.empty() &&
            h->gen_launched == h->gen_used + 1;
 }
 
@@ -1401,6 +1434,14 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "znt_stores") h->nt_stores = value != 0;
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
+    else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "halo_loopback") {
+        if (!h->comm || h->world != 1 || value < 0 || value > 2)
+            return fail(DF_EINVAL, "halo_loopback needs a one-rank RCCL handle (comm_id, world 1) and a value 0-2");
+        int rc;
+        if (value && !h->send_l && (rc = alloc_halo(h))) return rc;
+        h->halo_loopback = value;
+    }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "graph") h->use_graph = value != 0;
     else if (k == "ywin_T" || k == "zwin_T") {

@@ -677,6 +677,52 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
+#if !defined(DF_YPASS_NOWINDOW)
+    if (TABLE && !PC && YU < 4 && Nlo == Nhi && a.ywindow && t + 5 <= bh) {
+        // Table mode, one N for the whole tile (every tile of a row-uniform plane except where N
+        // steps): tap t of row r uses b[t - r], so the 4 taps t..t+3 of all R rows need only the
+        // R + 3 coefficients b[t-R+1 .. t+3], one s_load_dwordx16 window; the next iteration's
+        // window is loaded one iteration ahead so the scalar loads never stall the taps.
+        // Same products, same order: bit-identical to the per-row path.
+        constexpr int WN = (R + 3 + 7) / 8 * 8;
+        const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
+        double cw[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) cw[k] = cb[t + k];
+        double2 n0 = noise(t), n1 = noise(t + 1);
+        auto tap = [&](int u, const double2 n) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double b = cw[u - r + R - 1];
+                acc0[r] += b * n.x;
+                acc1[r] += b * n.y;
+            }
+        };
+        for (; t + 5 <= bh; t += 4) {
+            double cn[WN];
+#pragma unroll
+            for (int k = 0; k < WN; ++k) cn[k] = cb[t + 4 + k]; // the table is padded past its last vector
+            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
+            tap(0, n0);
+            tap(1, n1);
+            n0 = noise(t + 4);
+            n1 = noise(t + 5);
+            tap(2, m0);
+            tap(3, m1);
+#pragma unroll
+            for (int k = 0; k < WN; ++k) cw[k] = cn[k];
+        }
+        // t + 1 <= bh still holds (n0, n1 are rows t, t + 1): finish in the per-row loops below
+        for (; t + 1 <= bh; t += 2) {
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            if (t + 3 <= bh) {
+                n0 = noise(t + 2);
+                n1 = noise(t + 3);
+            }
+        }
+    }
+#endif
     if (kPrefetch && TABLE && !PC && YU < 4 && t + 1 <= bh) {
         // VALU-bound table mode: the next two noise rows are in flight while this pair's
         // taps run (the compiler would wait on each iteration's own loads)
@@ -1150,6 +1196,24 @@ hipError_t launch_gather(const double *src, long long nsrc, long long n, const l
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st)
 {
     hipLaunchKernelGGL(halo_pack_kernel, dim3(512), dim3(256), 0, st, a, send_l, send_r);
+    return hipGetLastError();
+}
+
+// One-rank RCCL loopback (tuning key halo_loopback): the halo columns a rank sent to itself must
+// arrive unchanged; mismatches are counted into *bad. corrupt = 1 perturbs element 0 as received
+// (a test of the check itself).
+__global__ void halo_check_kernel(const double *__restrict__ sent, const double *__restrict__ got, size_t n, int corrupt,
+                                  int *bad)
+{
+    for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
+        const double g = got[e] + ((corrupt && e == 0) ? 1.0 : 0.0);
+        if (g != sent[e] && !(g != g && sent[e] != sent[e])) atomicAdd(bad, 1);
+    }
+}
+
+hipError_t launch_halo_check(const double *sent, const double *got, size_t n, int corrupt, int *bad, hipStream_t st)
+{
+    hipLaunchKernelGGL(halo_check_kernel, dim3(256), dim3(256), 0, st, sent, got, n, corrupt, bad);
     return hipGetLastError();
 }
 

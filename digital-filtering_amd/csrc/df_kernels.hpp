@@ -93,6 +93,7 @@ struct SweepArgs {
     int nt_stores;          // z-pass outputs stored non-temporally
     int ynt_stores;         // y-pass output (r_zs) stored non-temporally
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
+    int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is
     // in the first W ticks of a T-tick period, so the CUs write together and the read stream runs
@@ -125,5 +126,6 @@ hipError_t launch_gather(const double *src, long long nsrc, long long n, const l
                          const long long *didx, long long ndst, double beta, int *bad, hipStream_t st);
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st);
 hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st);
+hipError_t launch_halo_check(const double *sent, const double *got, size_t n, int corrupt, int *bad, hipStream_t st);
 
 } // namespace dfamd

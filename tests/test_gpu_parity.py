@@ -361,6 +361,32 @@ def test_rccl_single_rank_matches_plain():
     plain.close()
 
 
+def test_rccl_halo_send_recv_loopback():
+    # The z-strip halo exchange (grouped ncclSend/ncclRecv of the packed edge columns, all three
+    # components) on one GPU: a one-rank communicator sends both plane edges to itself each call and
+    # the device compares what arrived with what was sent. Fields stay bit-identical to the plain
+    # handle (the received columns are not unpacked); a corrupted element must be reported.
+    spec = dict(plane="synthetic", Ny=96, Nz=300, N_min=4, N_max=16, seed=9, device=0)
+    plain = dfamd.DigitalFilter(**spec)
+    rc = dfamd.DigitalFilter(rank=0, world=1, comm_id=dfamd.comm_unique_id(), **spec)
+    with pytest.raises(dfamd.DFError):
+        plain.set_tuning("halo_loopback", 1)  # needs a communicator
+    rc.set_tuning("halo_loopback", 1)
+    for dt in (1e-8, 1e-8):
+        plain.filter(dt)
+        rc.filter(dt)
+    rc.sync()
+    for k in FIELDS:
+        assert np.array_equal(rc.field(k), plain.field(k)), k
+    assert rc.rng_state() == plain.rng_state()
+    rc.set_tuning("halo_loopback", 2)  # one received value perturbed: the check must see it
+    rc.filter(1e-8)
+    with pytest.raises(dfamd.DFError, match="loopback"):
+        rc.sync()
+    rc.close()
+    plain.close()
+
+
 def test_set_rng_state_discards_prefetched_noise():
     # The next call's noise is generated ahead of time on a second stream; moving the
     # stream must regenerate it (df.cpp:334-335 semantics: draws follow the state).

@@ -49,6 +49,8 @@ def parse():
                    help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
     p.add_argument("--cpu-calls", type=int, default=16)  # ~13 s of reference CPU work (0.8 s per call)
     p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--other-configs", default="c2",
+                   help="comma list of further single-GPU configs timed after the main one (N=1 only; '' = none)")
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
                    help="also time the other coefficient mode (N=1 only) and report it under alt_modes")
     return p.parse_args()
@@ -222,6 +224,41 @@ def main():
                                                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
                                                    "traffic_source": os.path.relpath(args.pmc_file, ROOT)}
 
+    others = None
+    if world == 1 and args.other_configs:
+        # BASELINE configs[1] (c2, 512 x 512, N 4-32) and any others, same mode, same timing rule
+        others = {}
+        for name in filter(None, args.other_configs.split(",")):
+            if name == args.config or name not in CONFIGS:
+                continue
+            oNy, oNz, olo, ohi, odesc = CONFIGS[name]
+            h = dfamd.DigitalFilter(plane="synthetic", Ny=oNy, Nz=oNz, N_min=olo, N_max=ohi, seed=args.seed,
+                                    device=local_rank, coeff_mode=args.coeff_mode, rows_per_wave=args.rows_per_wave)
+            for _ in range(args.warmup):
+                h.filter(args.dt)
+            h.sync()
+            h.set_profiling(True)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                h.filter(args.dt)
+            h.sync()
+            torch.cuda.synchronize()
+            el3 = time.perf_counter() - t1
+            p3 = h.profile()
+            ph = {"ypass": p3["ypass_ms"], "zpass": p3["zpass_ms"]}
+            d = max(ph, key=ph.get)
+            d_ms = ph[d] / max(1, p3["calls"])
+            d_ach = h.algorithmic_bytes(0 if d == "ypass" else 1) / (d_ms * 1e-3) / 1e9
+            others[name] = {"workload": odesc, "value": round(oNy * oNz * args.steps / el3, 1),
+                            "ms_per_step": round(el3 * 1e3 / args.steps, 4),
+                            "phase_ms_per_call": {k: round(p3[k] / max(1, p3["calls"]), 4)
+                                                  for k in ("rng_ms", "ypass_ms", "zpass_ms", "total_ms")},
+                            "roofline": ({"kernel": f"{d}_kernel", "achieved": round(d_ach, 1), "unit": "GB/s",
+                                          "frac": round(d_ach / HBM_PEAK_GBPS, 4)}
+                                         if args.coeff_mode == "packed" else None)}
+            h.close()
+
     out = None
     if rank == 0:
         cpu = None
@@ -254,6 +291,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "alt_modes": alt,
+            "other_configs": others,
             "setup_s": round(t_setup, 3),
         }
         print(json.dumps(out), flush=True)

@@ -121,21 +121,26 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        f.filter(args.dt)
-    f.sync()
-    f.set_profiling(True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        f.filter(args.dt)
-    f.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = f.profile()
-    f.set_profiling(False)
+    def timed(h):
+        """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile."""
+        for _ in range(args.warmup):
+            h.filter(args.dt)
+        h.sync()
+        h.set_profiling(True)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            h.filter(args.dt)
+        h.sync()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        prof = h.profile()
+        h.set_profiling(False)
+        return el, prof
+
+    elapsed, prof = timed(f)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -182,18 +187,7 @@ def main():
         g = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=args.seed,
                                 device=local_rank, coeff_mode=other, rows_per_wave=args.rows_per_wave)
         taps = sum(g.comp_info(c)["by_size"] + g.comp_info(c)["bz_size"] for c in range(3))
-        for _ in range(args.warmup):
-            g.filter(args.dt)
-        g.sync()
-        g.set_profiling(True)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            g.filter(args.dt)
-        g.sync()
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t1
-        p2 = g.profile()
+        el2, p2 = timed(g)
         g.close()
         ms2 = el2 * 1e3 / args.steps
         pm = load_pmc()
@@ -234,18 +228,7 @@ def main():
             oNy, oNz, olo, ohi, odesc = CONFIGS[name]
             h = dfamd.DigitalFilter(plane="synthetic", Ny=oNy, Nz=oNz, N_min=olo, N_max=ohi, seed=args.seed,
                                     device=local_rank, coeff_mode=args.coeff_mode, rows_per_wave=args.rows_per_wave)
-            for _ in range(args.warmup):
-                h.filter(args.dt)
-            h.sync()
-            h.set_profiling(True)
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                h.filter(args.dt)
-            h.sync()
-            torch.cuda.synchronize()
-            el3 = time.perf_counter() - t1
-            p3 = h.profile()
+            el3, p3 = timed(h)
             ph = {"ypass": p3["ypass_ms"], "zpass": p3["zpass_ms"]}
             d = max(ph, key=ph.get)
             d_ms = ph[d] / max(1, p3["calls"])

@@ -35,6 +35,12 @@ __device__ __forceinline__ double2 ld_pair(lds_pair_ptr p)
 #else
 #define DF_NOISE(ptr, tag) ld_pair(ptr)
 #endif
+// DF_ABLATE_TCOEF: table-mode coefficients become an inline constant (no scalar loads).
+#if defined(DF_ABLATE_TCOEF)
+#define DF_TCOEF(x) 0.5
+#else
+#define DF_TCOEF(x) (x)
+#endif
 
 // Coefficient stream load: read once per call, so optionally non-temporal.
 template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
@@ -591,11 +597,11 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         if (TABLE) {
             const int i = t - r;
             if (!PC) {
-                const double b = tb[r][i];
+                const double b = DF_TCOEF(tb[r][i]);
                 return make_double2(b, b);
             }
             const int ai = i < 0 ? -i : i;
-            return make_double2(tb[r][ai], tb1[r][ai]);
+            return make_double2(DF_TCOEF(tb[r][ai]), DF_TCOEF(tb1[r][ai]));
         }
         return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
     };
@@ -688,7 +694,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
         double cw[WN];
 #pragma unroll
-        for (int k = 0; k < WN; ++k) cw[k] = cb[t + k];
+        for (int k = 0; k < WN; ++k) cw[k] = DF_TCOEF(cb[t + k]);
         double2 n0 = noise(t), n1 = noise(t + 1);
         auto tap = [&](int u, const double2 n) {
 #pragma unroll
@@ -701,7 +707,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         for (; t + 5 <= bh; t += 4) {
             double cn[WN];
 #pragma unroll
-            for (int k = 0; k < WN; ++k) cn[k] = cb[t + 4 + k]; // the table is padded past its last vector
+            for (int k = 0; k < WN; ++k) cn[k] = DF_TCOEF(cb[t + 4 + k]); // the table is padded past its last vector
             const double2 m0 = noise(t + 2), m1 = noise(t + 3);
             tap(0, n0);
             tap(1, n1);
@@ -890,11 +896,11 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         auto coef = [&](int t) -> double2 {
             if (TABLE) {
                 if (!PC) {
-                    const double v = tb[t];
+                    const double v = DF_TCOEF(tb[t]);
                     return make_double2(v, v);
                 }
                 const int i = t - N, ai = i < 0 ? -i : i;
-                return make_double2(tb[ai], tb1[ai]);
+                return make_double2(DF_TCOEF(tb[ai]), DF_TCOEF(tb1[ai]));
             }
             return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
         };

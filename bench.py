@@ -173,6 +173,15 @@ def main():
                 "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 4)}
     if traffic_src:
         roofline["traffic_source"] = traffic_src
+    # measured stream ceilings of this GPU model (tools/hbm_probe: 8 GiB grid-stride kernels)
+    probe = os.path.join(ROOT, "profiles", "r1", "hbm_probe.json")
+    if os.path.exists(probe):
+        hp = json.load(open(probe))
+        ceil = hp.get("read_nt_g8192_GBps")
+        if ceil:
+            roofline["measured_ceiling"] = {"nt_read_GBps": ceil, "copy_GBps": hp.get("copy_GBps"),
+                                            "frac": round(achieved / ceil, 4),
+                                            "source": os.path.relpath(probe, ROOT)}
 
     def load_pmc():
         try:

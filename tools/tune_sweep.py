@@ -24,12 +24,15 @@ def main():
     ap.add_argument("--mode", default="packed")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=20)
+    ap.add_argument("--comm", action="store_true",
+                    help="one-rank RCCL handle (world 1 with a communicator): halo_loopback/halo_overlap apply")
     ap.add_argument("settings", nargs="+")
     a = ap.parse_args()
     if a.plane in SYN:
         Ny, Nz, lo, hi = SYN[a.plane]
+        extra = dict(rank=0, world=1, comm_id=dfamd.comm_unique_id()) if a.comm else {}
         f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=lo, N_max=hi, seed=1, device=0,
-                                coeff_mode=a.mode)
+                                coeff_mode=a.mode, **extra)
     else:
         f = dfamd.DigitalFilter(plane=a.plane, seed=1, device=0, coeff_mode=a.mode)
     sets = [[(kv.split("=")[0], int(kv.split("=")[1])) for kv in s.split(",") if kv] for s in a.settings]

@@ -49,8 +49,9 @@ def parse():
                    help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
     p.add_argument("--cpu-calls", type=int, default=16)  # ~13 s of reference CPU work (0.8 s per call)
     p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--other-configs", default="c2",
-                   help="comma list of further single-GPU configs timed after the main one (N=1 only; '' = none)")
+    p.add_argument("--other-configs", default="",
+                   help="comma list of further single-GPU configs timed after the main one (N=1 only), e.g. c2; "
+                        "off by default so that rocprofv3 averages of the default command cover c3 launches only")
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
                    help="also time the other coefficient mode (N=1 only) and report it under alt_modes")
     return p.parse_args()

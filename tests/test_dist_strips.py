@@ -1,4 +1,4 @@
-"""Multi-process z-strip decomposition on CPU (torch.distributed, gloo, world 2-3).
+"""Multi-process z-strip decomposition on CPU (torch.distributed, gloo, world 2-4).
 
 Each rank takes its column range [z0, z1) from the product's own planner (a
 host-only libdfamd handle, device = -1), restates the strip-local y-pass and the
@@ -109,7 +109,7 @@ def _worker(rank, world, port, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_gloo_z_strips_reproduce_single_plane(world):
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()

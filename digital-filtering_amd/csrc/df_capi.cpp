@@ -527,7 +527,8 @@ int write_csv_if(df_handle *h)
 
 // ---------------------------------------------------------------- create
 
-int build(df_handle *h, const df_config_c *cfg)
+// Config fields and the environment's tuning knobs (df.hpp:38-49 plus extensions).
+int read_config(df_handle *h, const df_config_c *cfg)
 {
     h->flow.d_i = cfg->d_i;
     h->flow.rho_e = cfg->rho_e;
@@ -575,11 +576,13 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
         h->rows_per_wave != 8)
         return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
+    return DF_OK;
+}
 
-    std::string err;
-    if (!build_setup(h->flow, h->spec, h->setup, err)) return fail(DF_EIO, err);
-    Setup &s = h->setup;
-
+// This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
+int plan_strips(df_handle *h)
+{
+    const Setup &s = h->setup;
     // ---- partition (host)
     h->Ny = s.Ny;
     h->Nz_g = s.Nz;
@@ -644,7 +647,14 @@ int build(df_handle *h, const df_config_c *cfg)
         }
     }
 
-    // ---- RNG stream geometry (df.cpp:343-348 order) and launch size
+    return DF_OK;
+}
+
+// RNG stream geometry (df.cpp:343-348 order) and launch size.
+int plan_rng(df_handle *h)
+{
+    const Setup &s = h->setup;
+    const int Ny = s.Ny;
     RngGeom &g = h->geom;
     g.seg[0] = 0;
     for (int c = 0; c < 3; ++c) {
@@ -691,16 +701,16 @@ int build(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_GEN_SPLIT")) g.gen_split = std::atoi(e);
     if (g.gen_split < 1 || g.gen_split > kRngPerThread || (g.gen_split & (g.gen_split - 1)))
         return fail(DF_EINVAL, "gen_split must be a power of two <= 16");
-    if (cfg->device < 0) { // host-only handle: setup queries, no GPU
-        h->device = -1;
-        return DF_OK;
-    }
+    return DF_OK;
+}
 
-    // ---- device
+// Device, streams and the noise-set events.
+int open_device(df_handle *h, int device)
+{
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(DF_EHIP, "no HIP device visible");
-    if (cfg->device >= ndev) return fail(DF_EINVAL, "device ordinal out of range");
-    h->device = cfg->device;
+    if (device >= ndev) return fail(DF_EINVAL, "device ordinal out of range");
+    h->device = device;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     // Sweeps on the high-priority queue, noise for the next call on the low one:
     // the memory-bound sweeps keep their waves; the compute-bound RNG fills gaps.
@@ -714,8 +724,15 @@ int build(df_handle *h, const df_config_c *cfg)
         HIP_OR(hipEventCreateWithFlags(&h->ev_rng[set], hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], hipEventDisableTiming), DF_EHIP);
     }
+    return DF_OK;
+}
 
-    // ---- per-N coefficient table
+// Per-N coefficient tables (table mode, and the source K0 expands the packed stream from) and the
+// per-row constants of apply_RST_scaling / get_rho_T_fluc.
+int upload_tables(df_handle *h)
+{
+    const Setup &s = h->setup;
+    const int Ny = s.Ny;
     std::vector<int> tab_off_h;
     std::vector<double> tab_h;
     int Nmax_all = 0;
@@ -767,9 +784,15 @@ int build(df_handle *h, const df_config_c *cfg)
         rowc[6 * Ny + j] = s.rhos[j];
     }
     if ((rc = dalloc_t(h, &h->rowc, rowc.size()))) return rc;
-    if ((rc = upload(h, h->rowc, rowc.data(), rowc.size()))) return rc;
+    return upload(h, h->rowc, rowc.data(), rowc.size());
+}
 
-    // ---- per-component buffers
+// Noise sets, fields, tap ranges and (packed mode) the strip-tap-major coefficient stream.
+int alloc_components(df_handle *h)
+{
+    const Setup &s = h->setup;
+    const int Ny = s.Ny;
+    int rc;
     const size_t n_loc = (size_t)Ny * h->Nz_loc;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -835,8 +858,14 @@ int build(df_handle *h, const df_config_c *cfg)
         }
     }
     if ((rc = dalloc_t(h, &h->T, n_loc))) return rc;
-    if ((rc = dalloc_t(h, &h->rho, n_loc))) return rc;
+    return dalloc_t(h, &h->rho, n_loc);
+}
 
+// RNG buffers, Brown jump tables, the error flags and the stream's starting state.
+int alloc_rng(df_handle *h, const df_config_c *cfg)
+{
+    RngGeom &g = h->geom;
+    int rc;
     for (int c = 0; c < 3; ++c) {
         g.Nzp[c] = h->c[c].Nzp;
         g.rz_pitch[c] = h->c[c].rz_pitch;
@@ -883,9 +912,13 @@ int build(df_handle *h, const df_config_c *cfg)
     if (cfg->seed_from_random_device) seed = (uint64_t)std::random_device{}(); // df.cpp:334
     RngStateDev st0{pcg_seed1(seed), 0, 0, 0.0};
     if (cfg->rng_resume) st0 = RngStateDev{cfg->rng_state, cfg->rng_saved_flag ? 1 : 0, 0, cfg->rng_saved};
-    if ((rc = upload(h, h->rstate, &st0, 1))) return rc;
+    return upload(h, h->rstate, &st0, 1);
+}
 
-    // ---- halo buffers + communicator
+// Halo buffers and the RCCL communicators (cfg->comm_id).
+int open_comm(df_handle *h, const df_config_c *cfg)
+{
+    int rc;
     if (h->world > 1 && (rc = alloc_halo(h))) return rc;
     // A communicator of one rank is accepted too: the same init, split and grouped all-gather then run on a
     // single GPU (tests/test_gpu_parity.py::test_rccl_single_rank_matches_plain), the halo being a no-op.
@@ -896,6 +929,26 @@ int build(df_handle *h, const df_config_c *cfg)
         NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
         h->split_count = true;
     }
+    return DF_OK;
+}
+
+int build(df_handle *h, const df_config_c *cfg)
+{
+    int rc;
+    if ((rc = read_config(h, cfg))) return rc;
+    std::string err;
+    if (!build_setup(h->flow, h->spec, h->setup, err)) return fail(DF_EIO, err);
+    if ((rc = plan_strips(h))) return rc;
+    if ((rc = plan_rng(h))) return rc;
+    if (cfg->device < 0) { // host-only handle: setup queries, no GPU
+        h->device = -1;
+        return DF_OK;
+    }
+    if ((rc = open_device(h, cfg->device))) return rc;
+    if ((rc = upload_tables(h))) return rc;
+    if ((rc = alloc_components(h))) return rc;
+    if ((rc = alloc_rng(h, cfg))) return rc;
+    if ((rc = open_comm(h, cfg))) return rc;
     for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     return DF_OK;

@@ -83,6 +83,42 @@ def cpu_baseline(args, Ny, N_min, N_max):
             "s_per_call": dt}
 
 
+PAR_SCRIPT = r"""
+import json, sys, time
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+Ny, Nz, lo, hi, seed, dt, calls = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), \
+    int(sys.argv[6]), float(sys.argv[7]), int(sys.argv[8])
+o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=Ny, Nz=Nz, N_min=lo, N_max=hi, seed=seed)
+o.filter(dt)
+t0 = time.perf_counter()
+for _ in range(calls):
+    o.filter(dt)
+print(json.dumps({"s_per_call": (time.perf_counter() - t0) / calls}))
+"""
+
+
+def cpu_baseline_parallel(args, Ny, N_min, N_max):
+    """The oracle restatement built with OpenMP over the sweep rows (oracle/liboracle_omp.so; the
+    RNG stays serial as in the reference) on this host's cores: a multi-core CPU figure beside the
+    single-threaded reference. Not the reference; same bits (tests/test_oracle_openmp.py)."""
+    lib = os.path.join(ROOT, "oracle", "liboracle_omp.so")
+    if not os.path.exists(lib):
+        return None
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    env = dict(os.environ, ORACLE_LIB=lib, OMP_NUM_THREADS=str(threads))
+    nz = args.cpu_cols
+    out = subprocess.run([sys.executable, "-c", PAR_SCRIPT, os.path.join(ROOT, "oracle"), str(Ny), str(nz),
+                          str(N_min), str(N_max), str(args.seed), str(args.dt), str(args.cpu_calls)],
+                         env=env, capture_output=True, text=True, check=True, timeout=600)
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    return {"value": Ny * nz / rec["s_per_call"], "unit": "cells/s", "cores": threads, "kind": "port",
+            "sample": f"{Ny}x{nz} (as cpu_baseline), {args.cpu_calls} filter(dt) calls",
+            "s_per_call": rec["s_per_call"],
+            "note": "oracle restatement with OpenMP over the rows of the sweeps and elementwise steps "
+                    "(RNG serial); not the reference, which is single-threaded"}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,12 +290,16 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None
+        cpu = cpu_par = None
         if args.cpu_baseline == "auto" and world == 1:
             try:
                 cpu = cpu_baseline(args, Ny, N_min, N_max)
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": str(e)}
+            try:
+                cpu_par = cpu_baseline_parallel(args, Ny, N_min, N_max)
+            except Exception as e:
+                cpu_par = {"error": str(e)}
         per_call = {k: round(prof[k] / max(1, prof["calls"]), 4) for k in ("rng_ms", "ypass_ms", "halo_ms",
                                                                             "zpass_ms", "total_ms")}
         out = {
@@ -283,6 +323,7 @@ def main():
             "phase_ms_per_call": per_call,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_baseline_parallel": cpu_par,
             "alt_modes": alt,
             "other_configs": others,
             "setup_s": round(t_setup, 3),

@@ -485,6 +485,9 @@ void orc_filtering_sweeps(orc_df *df, int comp)
     orc_field *F = &df->F[comp];
     int Ny = df->Ny, Nz = df->Nz;
     int Nz_pad = F->Nz_max, Ny_pad = F->Ny_max;
+    /* rows are independent and every cell keeps the reference's tap order, so the OpenMP build
+       (liboracle_omp.so, bench.py's parallel CPU figure) returns the same bits */
+#pragma omp parallel for schedule(dynamic, 8)
     for (int j = 0; j < Ny; ++j) {
         long long r_idy = (long long)(j + Ny_pad) * Nz;
         long long r_idz = (long long)j * (Nz + 2 * Nz_pad) + Nz_pad;
@@ -498,6 +501,7 @@ void orc_filtering_sweeps(orc_df *df, int comp)
             r_idy++; r_idz++; idx++;
         }
     }
+#pragma omp parallel for schedule(dynamic, 8)
     for (int j = 0; j < Ny; ++j) {
         long long r_idz = (long long)j * (Nz + 2 * Nz_pad) + Nz_pad;
         int idx = j * Nz;
@@ -518,6 +522,7 @@ void orc_correlate_fields(orc_df *df, int comp)
     orc_field *F = &df->F[comp];
     double pi = 3.141592654;
     double alpha = exp(-pi * df->dt / F->Lt);
+#pragma omp parallel for
     for (int idx = 0; idx < df->n_cells; ++idx)
         F->filt[idx] = F->filt_old[idx] * sqrt(alpha) + F->filt[idx] * sqrt(1.0 - alpha);
 }
@@ -526,6 +531,7 @@ void orc_apply_RST_scaling(orc_df *df)
 {
     /* df.cpp:419-447 */
     orc_field *u = &df->F[0], *v = &df->F[1], *w = &df->F[2];
+#pragma omp parallel for
     for (int j = 0; j < df->Ny; ++j) {
         double b;
         if (df->R11[j] < 1e-10) b = 0.0;
@@ -544,6 +550,7 @@ void orc_apply_RST_scaling(orc_df *df)
 void orc_get_rho_T_fluc(orc_df *df)
 {
     /* df.cpp:470-485 */
+#pragma omp parallel for
     for (int j = 0; j < df->Ny; ++j) {
         double temp1 = -0.5 * (1.4 - 1) * df->Ms[j] * df->Ms[j] / df->Us[j];
         for (int k = 0; k < df->Nz; ++k) {

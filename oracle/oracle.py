@@ -11,7 +11,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 DATA = os.path.join(os.path.dirname(HERE), "digital-filtering_amd", "data")
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+LIB_PATH = os.environ.get("ORACLE_LIB") or os.path.join(HERE, "liboracle.so")  # ORACLE_LIB: liboracle_omp.so
 
 PLANE_NATIVE, PLANE_SYNTHETIC, PLANE_GRID = 0, 1, 2
 

@@ -255,6 +255,13 @@ def main():
                                            "frac": round(flops / (sw_ms * 1e-3) / 1e12 / 78.6, 4),
                                            "flops_per_call": flops, "sweeps_ms": round(sw_ms, 4),
                                            "note": "mul+add without FMA contraction caps at 39.3 TFLOP/s"}
+            vp = os.path.join(ROOT, "profiles", "r1", "probe", "valu_probe_fp64.jsonl")
+            if os.path.exists(vp):  # measured FP64 mul+add issue ceiling of this GPU model (tools/valu_probe)
+                best = max(json.loads(l)["wave_instr_per_s"] for l in open(vp) if l.startswith("{"))
+                ceil_tf = best * 64 / 1e12  # one flop per lane per v_mul_f64 / v_add_f64
+                rv = alt[other]["roofline_valu"]
+                rv["measured_ceiling"] = {"TFLOPs": round(ceil_tf, 1), "frac": round(rv["achieved"] / ceil_tf, 4),
+                                          "source": os.path.relpath(vp, ROOT)}
             if all(m is not None for m in meas):
                 sweeps_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
                 ach = sum(meas) / (sweeps_ms * 1e-3) / 1e9

@@ -38,10 +38,15 @@ int fail(int code, const std::string &msg)
     return code;
 }
 
+// On failure the HIP error is also cleared from the thread's last-error slot, so that a later, healthy
+// launch check (hipGetLastError) does not report it again.
 #define HIP_OR(expr, code)                                                                                  \
     do {                                                                                                    \
         hipError_t e_ = (expr);                                                                             \
-        if (e_ != hipSuccess) return fail(code, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+        if (e_ != hipSuccess) {                                                                             \
+            (void)hipGetLastError();                                                                        \
+            return fail(code, std::string(#expr) + ": " + hipGetErrorString(e_));                          \
+        }                                                                                                   \
     } while (0)
 
 #define NCCL_OR(expr)                                                                                       \
@@ -148,9 +153,12 @@ int dalloc(df_handle *h, void **p, size_t bytes)
 {
     if (bytes == 0) bytes = 16;
     hipError_t e = hipMalloc(p, bytes);
-    if (e != hipSuccess)
+    if (e != hipSuccess) {
+        (void)hipGetLastError(); // HIP keeps the failure as the thread's last error: the next launch check
+                                 // (hipGetLastError after a kernel) would report it as its own
         return fail(e == hipErrorOutOfMemory ? DF_ENOMEM : DF_EHIP,
                     "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    }
     h->allocs.push_back(*p);
     HIP_OR(hipMemsetAsync(*p, 0, bytes, h->stream), DF_EHIP);
     return DF_OK;
@@ -1176,6 +1184,7 @@ df_handle *df_create(const df_config_c *cfg)
     }
     df_handle *h = new df_handle();
     int rc = DF_OK;
+    if (cfg->device >= 0) (void)hipGetLastError(); // a stale error of earlier HIP work is not this handle's
     if (cfg->device < 0 && cfg->world > 1 && !cfg->comm_id) rc = DF_OK; // host-only strip planning
     else if (cfg->world > 1 && !cfg->comm_id && !(std::getenv("DFAMD_SOLO_STRIP") && std::atoi(std::getenv("DFAMD_SOLO_STRIP"))))
         rc = fail(DF_EINVAL, "world > 1 needs comm_id (RCCL) or df_create_group (in-process strips)");

@@ -216,3 +216,18 @@ def test_extreme_aspect_planes(spec):
         assert g.rng_state() == o.rng.state
         for k in ("u", "v", "w", "T", "rho"):
             assert float(rel_err(g.field(k), o.field(k)).max()) <= 1e-6, k
+
+
+def test_plane_beyond_hbm_packed_fails_cleanly_table_runs():
+    """Maximum sizes: 12000 x 12000 at N 4-64 needs ~710 GB of packed coefficients, beyond one
+    MI355X's 288 GB. df_create must fail with the allocation named (no partial handle, nothing
+    leaked: the same plane is created right after), and the plane runs in table mode (~45 GB)."""
+    spec = dict(plane="synthetic", Ny=12000, Nz=12000, N_min=4, N_max=64, seed=8, device=0)
+    with pytest.raises(dfamd.DFError, match="hipMalloc"):
+        dfamd.DigitalFilter(coeff_mode="packed", **spec)
+    g = dfamd.DigitalFilter(coeff_mode="table", **spec)
+    g.filter(1e-8)
+    u = g.field("u")
+    assert u.shape == (12000, 12000) and np.isfinite(u).all() and float(np.abs(u).max()) > 0
+    assert g.rng_state() != O.Rng(seed=8).state
+    g.close()

@@ -543,3 +543,40 @@ def test_random_planes_vs_oracle(case):
         for k in FIELDS:
             got = np.concatenate([h.field(k) for h in hs], axis=1)
             assert float(rel_err(got, o.field(k)).max()) <= TOL, (dt, k)
+
+
+def test_handles_driven_from_two_host_threads():
+    # No hidden process-wide state in the library (the reference's RNG is a process-wide static,
+    # df.cpp:334-335; here each handle owns its stream): two handles filtered concurrently from two
+    # host threads (ctypes drops the GIL in each call) give exactly the single-threaded results.
+    import threading
+
+    specs = [dict(plane="synthetic", Ny=300, Nz=260, N_min=2, N_max=24, seed=s, device=0) for s in (31, 32)]
+    ref = []
+    for sp in specs:
+        f = dfamd.DigitalFilter(**sp)
+        for _ in range(5):
+            f.filter(1e-8)
+        ref.append({k: f.field(k) for k in FIELDS})
+        f.close()
+    hs = [dfamd.DigitalFilter(**sp) for sp in specs]
+    errs = []
+
+    def run(f):
+        try:
+            for _ in range(5):
+                f.filter(1e-8)
+            f.sync()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(f,)) for f in hs]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    for f, r in zip(hs, ref):
+        for k in FIELDS:
+            assert np.array_equal(f.field(k), r[k]), k
+        f.close()

@@ -490,6 +490,77 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     }
 }
 
+// K2 + K2c in one block for planes of at most 1024 attempt blocks (c1, c2, the reference's own
+// grid): the scan of the block counts (one count per thread), the attempt-shortage check and the
+// wave plan, with the offsets kept in LDS. One launch instead of three: small planes are bound by
+// the host's launch rate. Same offsets, part[0] = 0 and task list as K2a/K2b/K2c (task order is
+// free: K3 takes its ranks from each task).
+__global__ __launch_bounds__(1024) void rng_scan_plan_small_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                   const int *__restrict__ counts,
+                                                                   long long *__restrict__ offsets,
+                                                                   long long *__restrict__ part,
+                                                                   const int *__restrict__ wave_counts, int nb_scan,
+                                                                   int nb_total, WaveTask *__restrict__ tasks,
+                                                                   int *__restrict__ ntasks, int *__restrict__ err)
+{
+    constexpr int WPB = kRngThreads / 64;
+    __shared__ long long p[1024];
+    __shared__ int base_sh;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int v = tid < nb_scan ? counts[tid] : 0;
+    p[tid] = v;
+    if (tid == 0) base_sh = 0;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) { // inclusive scan
+        const long long y = tid >= o ? p[tid - o] : 0;
+        __syncthreads();
+        p[tid] += y;
+        __syncthreads();
+    }
+    const long long excl = p[tid] - v;
+    if (tid < nb_scan) offsets[tid] = excl;
+    __syncthreads();
+    p[tid] = excl; // exclusive offsets for the plan below
+    __syncthreads();
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    if (tid == 0) {
+        part[0] = 0;
+        if (p[nb_scan - 1] + counts[nb_scan - 1] < A) *err = 1; // not enough attempts launched
+        if (f) {
+            double *d = stream_dest(g, stream_pos(g, 0));
+            if (d) *d = sin->saved * 1.0 + 0.0;
+        }
+    }
+    for (int gw0 = 0; gw0 < nb_total * WPB; gw0 += 1024) { // uniform trip count: every wave reaches the barriers
+        const int gw = gw0 + tid;
+        bool need = false;
+        long long r_lo = 0;
+        if (gw < nb_total * WPB) {
+            const int b = gw / WPB, w = gw % WPB;
+            r_lo = p[b];
+            for (int ww = 0; ww < w; ++ww) r_lo += wave_counts[(size_t)b * WPB + ww];
+            const long long r_hi = r_lo + wave_counts[gw];
+            if (r_lo < A) {
+                const uint64_t q_lo = f + 2ull * (uint64_t)r_lo;
+                const uint64_t q_hi = (f + 2ull * (uint64_t)r_hi) < g.Q ? (f + 2ull * (uint64_t)r_hi) : g.Q;
+                const bool ends_call = A - 1 < r_hi;
+                need = ends_call || (q_lo < q_hi && range_needed(g, q_lo, q_hi));
+            }
+        }
+        const uint64_t m = __ballot(need);
+        int base = 0;
+        if (m && lane == 0) base = atomicAdd(&base_sh, __popcll(m)); // LDS atomic: one block
+        base = __shfl(base, 0);
+        if (need) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            tasks[base + below] = WaveTask{r_lo, gw, 0};
+        }
+    }
+    __syncthreads();
+    if (tid == 0) *ntasks = base_sh;
+}
+
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
@@ -503,11 +574,21 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
                              WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st)
 {
     const int nparts = (nb_scan + 1023) / 1024; // <= 1024: checked at create
-    hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
-    hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err, ntasks);
-    const int nw = nb_total * (kRngThreads / 64);
-    hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part, wave_counts,
-                       nb_total, tasks, ntasks);
+#if defined(DF_NO_SMALL_SCAN)
+    constexpr bool small_ok = false; // timing-only variant: always the three-kernel form
+#else
+    constexpr bool small_ok = true;
+#endif
+    if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {
+        hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
+                           wave_counts, nb_scan, nb_total, tasks, ntasks, err);
+    } else {
+        hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
+        hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err, ntasks);
+        const int nw = nb_total * (kRngThreads / 64);
+        hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part,
+                           wave_counts, nb_total, tasks, ntasks);
+    }
     hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in, st_out,
                        tasks, ntasks, masks);
     return hipGetLastError();

@@ -97,6 +97,7 @@ struct df_handle {
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
+    int rng_replicate = 0; // z-strips: every rank counts every attempt block (no RNG all-gather)
     int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
@@ -579,7 +580,8 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GRAPH")) h->use_graph = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
-    if (h->solo_strip) h->split_count = true;
+    if (const char *e = std::getenv("DFAMD_RNG_REPLICATE")) h->rng_replicate = std::atoi(e) != 0;
+    if (h->solo_strip && !h->rng_replicate) h->split_count = true;
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
     if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
         h->rows_per_wave != 8)
@@ -935,7 +937,7 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         std::memcpy(&id, cfg->comm_id, sizeof(id));
         NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
         NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
-        h->split_count = true;
+        h->split_count = !h->rng_replicate;
     }
     return DF_OK;
 }
@@ -1497,6 +1499,11 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter
+        if (h->group) return fail(DF_EINVAL, "rng_replicate applies to RCCL or single handles, not in-process groups");
+        h->rng_replicate = value != 0;
+        h->split_count = (h->comm || h->solo_strip) && !h->rng_replicate;
+    }
     else if (k == "halo_loopback") {
         if (!h->comm || h->world != 1 || value < 0 || value > 2)
             return fail(DF_EINVAL, "halo_loopback needs a one-rank RCCL handle (comm_id, world 1) and a value 0-2");

@@ -5,56 +5,110 @@ One step = one filter(dt) call (reference df.cpp:449-468) over the whole plane:
 device RNG in the reference's stream order, y- and z-convolutions streaming the
 offset-packed coefficients, correlation, RST scaling, SRA T'/rho'.
 
-Workload (N=1): BASELINE configs[2] / SURVEY c3 — 2048 x 2048 plane, half-width
-rule N in [4, 64], dt = 1e-8, synthetic rows from files/RST.dat + line.dat.
-N>1 (weak scaling): one 2048 x 2048 z-strip per GPU of a 2048 x (2048 N) plane,
-one RCCL halo exchange per call (N=4 is SURVEY c4's 2048 x 8192 plane).
+Workloads (BASELINE.json configs; SURVEY 8d half-width rule, dt = 1e-8):
+  c3  2048 x 2048, N 4-64      configs[2], the HBM roofline point: the N = 1 default
+  c4  2048 x 8192, N 4-64      configs[3]: split into N z-strips, the N > 1 default
+  c5  4096 x 4096, N 4-64      configs[4]: split into N z-strips (reported beside c4 at N > 1)
+  c2  512 x 512, N 4-32        configs[1];  c1 128 x 128, N = 8 (configs[0], the CPU case)
+  native                       the reference's own 510 x 400 grid (df.cpp:71-118)
+--scaling strong (default) keeps the plane and splits it over the ranks; --scaling weak gives
+every rank the config's whole plane as its strip (plane Nz x N). Multi-GPU: one process per
+GPU, one RCCL halo exchange per call; after the timed region every rank re-runs the whole
+plane unsplit in table mode on its own GPU and compares its strip bit for bit (parity_ok).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--coeff-mode packed|table]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--coeff-mode packed|table]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
 import json
-import math
 import os
 import subprocess
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "digital-filtering_amd")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FIELDS = ("u", "v", "w", "T", "rho")
 
+# name: plane, Ny, Nz (whole plane), N_min, N_max, description
 CONFIGS = {
-    # name: (Ny, Nz per GPU, N_min, N_max, description)
-    "c1": (128, 128, 8, 8, "c1: 128x128 plane, constant half-width N=8"),
-    "c2": (512, 512, 4, 32, "c2: 512x512 plane, half-width 4-32"),
-    "c3": (2048, 2048, 4, 64, "c3: 2048x2048 plane per GPU, half-width 4-64 (HBM roofline point)"),
-    "c5": (4096, 4096, 4, 64, "c5: 4096x4096 plane per GPU, half-width 4-64"),
+    "c1": ("synthetic", 128, 128, 8, 8, "c1: 128x128 plane, constant half-width N=8"),
+    "c2": ("synthetic", 512, 512, 4, 32, "c2: 512x512 plane, half-width 4-32"),
+    "c3": ("synthetic", 2048, 2048, 4, 64, "c3: 2048x2048 plane, half-width 4-64 (HBM roofline point)"),
+    "c4": ("synthetic", 2048, 8192, 4, 64, "c4: 2048x8192 plane, half-width 4-64, z-strips over the GPUs"),
+    "c5": ("synthetic", 4096, 4096, 4, 64, "c5: 4096x4096 plane, half-width 4-64, z-strips over the GPUs"),
+    "native": ("native", 0, 0, 0, 0, "native: the reference's own 510x400 grid (read_grid, df.cpp:71-118)"),
 }
 
 
-def parse():
+def plan_workload(name, world, scaling="strong"):
+    """The plane one run times and each rank's z-strip [z0, z1) (df_capi.cpp plan_strips:
+    z0 = r*Nz/world). strong: the config's plane split over the ranks; weak: a plane Nz*world
+    wide, so every rank holds the config's Nz columns."""
+    plane, Ny, Nz, lo, hi, desc = CONFIGS[name]
+    if plane == "native":
+        if world > 1:
+            raise ValueError("the native grid is a single-GPU plane")
+        return {"name": name, "plane": plane, "Ny": 510, "Nz": 400, "N_min": 0, "N_max": 0, "desc": desc,
+                "scaling": "strong", "strips": [(0, 400)]}
+    if scaling not in ("strong", "weak"):
+        raise ValueError(scaling)
+    Nzg = Nz * world if scaling == "weak" else Nz
+    strips = [(r * Nzg // world, (r + 1) * Nzg // world) for r in range(world)]
+    if world > 1 and min(z1 - z0 for z0, z1 in strips) < hi:
+        raise ValueError(f"{name} over {world} GPUs: strips narrower than the z half-width {hi}")
+    if scaling == "weak" and world > 1:
+        desc = f"{desc.split(':')[0]} per GPU (weak): {Ny}x{Nzg} plane, {Ny}x{Nz} per GPU, half-width {lo}-{hi}"
+    return {"name": name, "plane": plane, "Ny": Ny, "Nz": Nzg, "N_min": lo, "N_max": hi, "desc": desc,
+            "scaling": scaling if world > 1 else "strong", "strips": strips}
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    p.add_argument("--config", default="auto", choices=["auto"] + sorted(CONFIGS),
+                   help="auto: c3 on one GPU, c4 split over N > 1 GPUs")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     p.add_argument("--coeff-mode", default="packed", choices=["packed", "table"])
     p.add_argument("--rows-per-wave", type=int, default=0)  # 0 = library default per mode
     p.add_argument("--dt", type=float, default=1e-8)
     p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--parity", default="on", choices=["on", "off"],
+                   help="after the timed region compare every rank's strip with the unsplit plane (table mode)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
     p.add_argument("--cpu-cols", type=int, default=512,
                    help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
     p.add_argument("--cpu-calls", type=int, default=16)  # ~13 s of reference CPU work (0.8 s per call)
     p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    p.add_argument("--other-configs", default="",
-                   help="comma list of further single-GPU configs timed after the main one (N=1 only), e.g. c2; "
-                        "off by default so that rocprofv3 averages of the default command cover c3 launches only")
+    p.add_argument("--other-configs", default="auto",
+                   help="comma list of further configs timed after the main one, same mode and rule; "
+                        "auto: 'native,c2' on one GPU, 'c5' on N > 1; '' for none")
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
                    help="also time the other coefficient mode (N=1 only) and report it under alt_modes")
-    return p.parse_args()
+    a = p.parse_args(argv)
+    return a
+
+
+def host_cpu():
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"host_cpu": model, "host_cores": os.cpu_count(), "host_cores_usable": usable,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
 def cpu_baseline(args, Ny, N_min, N_max):
@@ -69,18 +123,27 @@ def cpu_baseline(args, Ny, N_min, N_max):
         out = subprocess.run([exe, "time", run_root, str(args.seed), str(Ny), str(nz), str(N_min), str(N_max),
                               str(args.dt), str(args.cpu_calls)], capture_output=True, text=True, check=True)
         rec = json.loads(out.stdout.strip().splitlines()[-1])
-        return {"value": Ny * nz / rec["mean_s"], "unit": "cells/s", "cores": 1, "kind": "reference",
-                "sample": sample, "s_per_call": rec["mean_s"],
-                "stage_s": {k: rec[k] for k in ("noise_s", "sweeps_s", "correlate_s", "rst_s", "sra_s")}}
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=Ny, Nz=nz, N_min=N_min, N_max=N_max, seed=args.seed)
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_calls):
-        o.filter(args.dt)
-    dt = (time.perf_counter() - t0) / args.cpu_calls
-    return {"value": Ny * nz / dt, "unit": "cells/s", "cores": 1, "kind": "port", "sample": sample,
-            "s_per_call": dt}
+        res = {"value": Ny * nz / rec["mean_s"], "unit": "cells/s", "cores": 1, "kind": "reference",
+               "sample": sample, "s_per_call": rec["mean_s"],
+               "stage_s": {k: rec[k] for k in ("noise_s", "sweeps_s", "correlate_s", "rst_s", "sra_s")}}
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=Ny, Nz=nz, N_min=N_min, N_max=N_max, seed=args.seed)
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_calls):
+            o.filter(args.dt)
+        dt = (time.perf_counter() - t0) / args.cpu_calls
+        res = {"value": Ny * nz / dt, "unit": "cells/s", "cores": 1, "kind": "port", "sample": sample,
+               "s_per_call": dt}
+    res.update(host_cpu())
+    # BASELINE.md CPU plan step 5: the multi-GPU configs per cell from this sample (derived, not run)
+    res["extrapolated"] = {
+        name: {"cells": CONFIGS[name][1] * CONFIGS[name][2],
+               "s_per_call": round(CONFIGS[name][1] * CONFIGS[name][2] / res["value"], 3),
+               "derived": "cells / the sample's cells/s (per-cell cost is column-independent; same N rule)"}
+        for name in ("c4", "c5")}
+    return res
 
 
 PAR_SCRIPT = r"""
@@ -119,229 +182,327 @@ def cpu_baseline_parallel(args, Ny, N_min, N_max):
                     "(RNG serial); not the reference, which is single-threaded"}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
-        args.gpus = world
+class Ctx:
+    """Process-group plumbing: rank, world, device and the gather/reduce helpers."""
 
-    # torch first: libdfamd.so then binds to the same HIP runtime torch loaded.
-    import torch
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
 
-    sys.path.insert(0, PKG)
-    import dfamd
+    def init(self, torch, backend="nccl"):
+        """backend "nccl" (RCCL, the bench) or "gloo" (CPU tests of this plumbing)."""
+        self.torch = torch
+        if backend == "nccl":
+            torch.cuda.set_device(self.local_rank)
+        if self.world > 1:
+            import torch.distributed as dist
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+            else:
+                dist.init_process_group("gloo")
+            self.dist = dist
 
-    Ny, Nz_per, N_min, N_max, desc = CONFIGS[args.config]
-    Nz = Nz_per * world
-    comm_id = None
-    if world > 1:
-        obj = [dfamd.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
 
-    t_setup = time.perf_counter()
-    f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=args.seed,
-                            device=local_rank, rank=rank, world=world, comm_id=comm_id,
-                            coeff_mode=args.coeff_mode, rows_per_wave=args.rows_per_wave)
-    t_setup = time.perf_counter() - t_setup
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
+    def comm_id(self, dfamd):
+        if self.dist is None:
+            return None
+        obj = [dfamd.comm_unique_id() if self.rank == 0 else None]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
 
-    def timed(h):
-        """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile."""
-        for _ in range(args.warmup):
-            h.filter(args.dt)
-        h.sync()
-        h.set_profiling(True)
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            h.filter(args.dt)
-        h.sync()
-        torch.cuda.synchronize()
-        barrier()
-        el = time.perf_counter() - t0
-        prof = h.profile()
-        h.set_profiling(False)
-        return el, prof
 
-    elapsed, prof = timed(f)
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+def make_filter(dfamd, ctx, wl, args, coeff_mode, split=True, comm_id=None):
+    kw = dict(seed=args.seed, device=ctx.local_rank, coeff_mode=coeff_mode, rows_per_wave=args.rows_per_wave)
+    if wl["plane"] == "native":
+        return dfamd.DigitalFilter(plane="native", **kw)
+    kw.update(plane="synthetic", Ny=wl["Ny"], Nz=wl["Nz"], N_min=wl["N_min"], N_max=wl["N_max"])
+    if split and ctx.world > 1:
+        kw.update(rank=ctx.rank, world=ctx.world, comm_id=comm_id)
+    return dfamd.DigitalFilter(**kw)
 
-    cells_total = Ny * Nz
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = cells_total * args.steps / elapsed
 
-    # roofline of the dominant kernel, from hipEvents on the library's stream
+def timed(ctx, h, args):
+    """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile."""
+    torch = ctx.torch
+    for _ in range(args.warmup):
+        h.filter(args.dt)
+    h.sync()
+    h.set_profiling(True)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        h.filter(args.dt)
+    h.sync()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    el = time.perf_counter() - t0
+    prof = h.profile()
+    h.set_profiling(False)
+    return el, prof
+
+
+def per_call(prof):
+    return {k: round(prof[k] / max(1, prof["calls"]), 4) for k in ("rng_ms", "ypass_ms", "halo_ms", "zpass_ms",
+                                                                 "total_ms")}
+
+
+def compare(h, ref, z0, z1):
+    """Bit-for-bit comparison of this strip with the same columns of the unsplit plane."""
+    bad = {}
+    worst = 0.0
+    for k in FIELDS:
+        a = h.field(k)
+        b = np.ascontiguousarray(ref.field(k)[:, z0:z1])
+        n = int(np.count_nonzero(a.view(np.uint64) != b.view(np.uint64)))
+        if n:
+            bad[k] = n
+            worst = max(worst, float(np.nanmax(np.abs(a - b))))
+    rng_ok = h.rng_state() == ref.rng_state()
+    return {"ok": (not bad) and rng_ok, "mismatched_cells": bad, "max_abs_diff": worst, "rng_state_equal": rng_ok}
+
+
+def parity_check(dfamd, ctx, wl, args, h, calls, ref=None):
+    """This rank's strip after `calls` filter(dt) calls against the whole plane run unsplit in table mode
+    on this rank's own GPU (packed and table mode, any strip count: bit-identical by construction)."""
+    own = ref is None
+    if own:
+        ref = make_filter(dfamd, ctx, wl, args, "table", split=False)
+        for _ in range(calls):
+            ref.filter(args.dt)
+    z0, z1 = h.z0, h.z1
+    res = compare(h, ref, z0, z1)
+    if own:
+        ref.close()
+    res["rank"] = ctx.rank
+    res["columns"] = [z0, z1]
+    return res
+
+
+def roofline_of(h, prof, args, config_name):
     phase = {"ypass": prof["ypass_ms"], "zpass": prof["zpass_ms"]}
     dom = max(phase, key=phase.get)
     dom_ms = phase[dom] / max(1, prof["calls"])
-    alg = f.algorithmic_bytes(0 if dom == "ypass" else 1)
-    call_alg = f.algorithmic_bytes(-1)
+    alg = h.algorithmic_bytes(0 if dom == "ypass" else 1)
     achieved = alg / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    traffic_src = None
+    r = {"bound": "hbm", "kernel": f"{dom}_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+         "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 4)}
     if os.path.exists(args.pmc_file):
         try:
-            pm = json.load(open(args.pmc_file))
-            key = f"{args.config}/{args.coeff_mode}/{dom}"
-            if key in pm.get("per_launch_bytes", {}):
-                traffic = pm["per_launch_bytes"][key]
-                traffic_src = os.path.relpath(args.pmc_file, ROOT)
+            pm = json.load(open(args.pmc_file)).get("per_launch_bytes", {})
+            key = f"{config_name}/{args.coeff_mode}/{dom}"
+            if key in pm:
+                r["traffic"] = pm[key]
+                r["traffic_source"] = os.path.relpath(args.pmc_file, ROOT)
         except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "kernel": f"{dom}_kernel", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": round(dom_ms, 4)}
-    if traffic_src:
-        roofline["traffic_source"] = traffic_src
-    # measured stream ceilings of this GPU model (tools/hbm_probe: 8 GiB grid-stride kernels)
+            pass
     probe = os.path.join(ROOT, "profiles", "r1", "hbm_probe.json")
-    if os.path.exists(probe):
+    if os.path.exists(probe):  # measured stream ceilings of this GPU model (tools/hbm_probe)
         hp = json.load(open(probe))
         ceil = hp.get("read_nt_g8192_GBps")
         if ceil:
-            roofline["measured_ceiling"] = {"nt_read_GBps": ceil, "copy_GBps": hp.get("copy_GBps"),
-                                            "frac": round(achieved / ceil, 4),
-                                            "source": os.path.relpath(probe, ROOT)}
+            r["measured_ceiling"] = {"nt_read_GBps": ceil, "copy_GBps": hp.get("copy_GBps"),
+                                     "frac": round(achieved / ceil, 4), "source": os.path.relpath(probe, ROOT)}
+    return r
 
-    def load_pmc():
-        try:
-            return json.load(open(args.pmc_file)).get("per_launch_bytes", {})
-        except Exception:
-            return {}
+
+def run_config(dfamd, ctx, wl, args, comm_id):
+    """Create, time and parity-check one workload on every rank. Returns the rank-0 view."""
+    t_setup = time.perf_counter()
+    f = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
+    t_setup = time.perf_counter() - t_setup
+    elapsed, prof = timed(ctx, f, args)
+    rank_rec = {"rank": ctx.rank, "elapsed_s": elapsed, "phase_ms_per_call": per_call(prof),
+                "roofline": roofline_of(f, prof, args, wl["name"]), "columns": [f.z0, f.z1],
+                "comm": f.comm_info() if ctx.world > 1 else None, "setup_s": round(t_setup, 3),
+                "call_bytes": f.algorithmic_bytes(-1)}
+    return f, rank_rec
+
+
+def summarize(ctx, wl, args, recs):
+    """Whole-job numbers from every rank's record (max-over-ranks time)."""
+    el_max = max(r["elapsed_s"] for r in recs)
+    el_min = min(r["elapsed_s"] for r in recs)
+    cells = wl["Ny"] * wl["Nz"]
+    ms = el_max * 1e3 / args.steps
+    slowest = max(recs, key=lambda r: r["roofline"]["avg_launch_ms"])
+    out = {"value": round(cells * args.steps / el_max, 1), "ms_per_step": round(ms, 4),
+           "phase_ms_per_call": recs[0]["phase_ms_per_call"], "roofline": slowest["roofline"]}
+    if ctx.world > 1:
+        out["roofline"] = dict(slowest["roofline"], rank=slowest["rank"],
+                               frac_by_rank=[r["roofline"]["frac"] for r in recs])
+        cm = recs[0]["comm"] or {}
+        out["multi_gpu"] = {
+            "rccl_ranks": cm.get("rccl_ranks"),
+            "rng_collective": ("allgather(counts, wave counts, accept masks)" if cm.get("rng_collective")
+                               else "none: every rank counts the whole stream (replicated), halo is the only collective"),
+            "halo_ms_per_call": {"max": max(r["phase_ms_per_call"]["halo_ms"] for r in recs),
+                                 "min": min(r["phase_ms_per_call"]["halo_ms"] for r in recs)},
+            "halo_bytes_per_call": sum((r["comm"] or {}).get("halo_bytes_sent", 0) for r in recs),
+            "rng_collective_bytes_per_call": sum((r["comm"] or {}).get("rng_bytes_received", 0) for r in recs),
+            "rank_ms_per_step": {"min": round(el_min * 1e3 / args.steps, 4), "max": round(ms, 4)},
+            "per_rank": [{"rank": r["rank"], "columns": r["columns"],
+                          "ms_per_step": round(r["elapsed_s"] * 1e3 / args.steps, 4),
+                          "phase_ms_per_call": r["phase_ms_per_call"]} for r in recs],
+        }
+    return out
+
+
+def main(argv=None):
+    args = parse(argv)
+    ctx = Ctx()
+    if ctx.world != args.gpus:
+        if ctx.world == 1 and args.gpus > 1:
+            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
+        args.gpus = ctx.world
+    name = args.config if args.config != "auto" else ("c3" if ctx.world == 1 else "c4")
+    wl = plan_workload(name, ctx.world, args.scaling)
+    others_arg = args.other_configs
+    if others_arg == "auto":
+        others_arg = "native,c2" if ctx.world == 1 else "c5"
+
+    # torch first: libdfamd.so then binds to the same HIP runtime torch loaded.
+    import torch
+    ctx.init(torch)
+    sys.path.insert(0, PKG)
+    import dfamd
+
+    comm_id = ctx.comm_id(dfamd)
+    f, rec = run_config(dfamd, ctx, wl, args, comm_id)
+    recs = ctx.gather(rec)
+    head = summarize(ctx, wl, args, recs)
+    calls_done = 1 + args.warmup + args.steps  # constructor step 0 + warmup + timed
 
     alt = None
-    if world == 1 and args.alt_modes == "auto":
+    ref_for_parity = None
+    if ctx.world == 1 and args.alt_modes == "auto" and wl["plane"] != "native":
         other = "table" if args.coeff_mode == "packed" else "packed"
-        f.close()
-        g = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=args.seed,
-                                device=local_rank, coeff_mode=other, rows_per_wave=args.rows_per_wave)
+        g = make_filter(dfamd, ctx, wl, args, other)
         taps = sum(g.comp_info(c)["by_size"] + g.comp_info(c)["bz_size"] for c in range(3))
-        el2, p2 = timed(g)
-        g.close()
+        el2, p2 = timed(ctx, g, args)
         ms2 = el2 * 1e3 / args.steps
-        pm = load_pmc()
-        meas = [pm.get(f"{args.config}/{other}/{k}") for k in ("ypass", "zpass")]
-        alt = {other: {"value": round(cells_total * args.steps / el2, 1), "ms_per_step": round(ms2, 4),
-                       "phase_ms_per_call": {k: round(p2[k] / max(1, p2["calls"]), 4)
-                                             for k in ("rng_ms", "ypass_ms", "halo_ms", "zpass_ms", "total_ms")}}}
+        cells = wl["Ny"] * wl["Nz"]
+        alt = {other: {"value": round(cells * args.steps / el2, 1), "ms_per_step": round(ms2, 4),
+                       "phase_ms_per_call": per_call(p2)}}
         if other == "table":
-            alt[other]["note"] = ("same results bit for bit (tests/test_gpu_parity.py); coefficients read from a "
-                                  "per-N table instead of the 20.7 GB offset-packed stream, so SURVEY 8d's "
-                                  "algorithmic bytes do not apply: the roofline uses rocprofv3-measured bytes")
-            # Table mode is FP64-VALU bound: 2 flop (mul, add) per tap and cell (SURVEY 8d: 5.17 GFLOP at c3).
-            # Peak: MI355X FP64 vector 78.6 TFLOP/s (datasheet; half the guide's 157.3 FP32); the sums
-            # must not contract to FMA (bit-exactness), which caps mul+add at half of that.
+            ref_for_parity = g  # same seed, same calls: the unsplit table-mode reference of the parity check
+            alt[other]["note"] = ("same results bit for bit (parity below, tests/test_gpu_parity.py); coefficients "
+                                  "read from a per-N table instead of the offset-packed stream, so SURVEY 8d's "
+                                  "algorithmic bytes do not apply: FP64-VALU roofline below")
+            # 2 flop (mul, add) per tap and cell (SURVEY 8d: 5.17 GFLOP at c3). Peak: MI355X FP64 vector
+            # 78.6 TFLOP/s; the sums must not contract to FMA (bit-exactness), so mul+add caps at half.
             sw_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
             flops = 2.0 * taps
-            alt[other]["roofline_valu"] = {"bound": "valu-fp64", "achieved": round(flops / (sw_ms * 1e-3) / 1e12, 2),
-                                           "peak": 78.6, "unit": "TFLOP/s",
-                                           "frac": round(flops / (sw_ms * 1e-3) / 1e12 / 78.6, 4),
+            tf = flops / (sw_ms * 1e-3) / 1e12
+            alt[other]["roofline_valu"] = {"bound": "valu-fp64", "achieved": round(tf, 2), "peak": 78.6,
+                                           "unit": "TFLOP/s", "frac": round(tf / 78.6, 4),
                                            "flops_per_call": flops, "sweeps_ms": round(sw_ms, 4),
                                            "note": "mul+add without FMA contraction caps at 39.3 TFLOP/s"}
             vp = os.path.join(ROOT, "profiles", "r1", "probe", "valu_probe_fp64.jsonl")
-            if os.path.exists(vp):  # measured FP64 mul+add issue ceiling of this GPU model (tools/valu_probe)
+            if os.path.exists(vp):  # measured FP64 mul+add issue ceiling (tools/valu_probe)
                 best = max(json.loads(l)["wave_instr_per_s"] for l in open(vp) if l.startswith("{"))
-                ceil_tf = best * 64 / 1e12  # one flop per lane per v_mul_f64 / v_add_f64
-                rv = alt[other]["roofline_valu"]
-                rv["measured_ceiling"] = {"TFLOPs": round(ceil_tf, 1), "frac": round(rv["achieved"] / ceil_tf, 4),
-                                          "source": os.path.relpath(vp, ROOT)}
-            if all(m is not None for m in meas):
-                sweeps_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
-                ach = sum(meas) / (sweeps_ms * 1e-3) / 1e9
-                alt[other]["roofline_measured"] = {"bound": "hbm", "kernels": "ypass+zpass",
-                                                   "measured_bytes_per_call": sum(meas),
-                                                   "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                                                   "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                                                   "traffic_source": os.path.relpath(args.pmc_file, ROOT)}
+                ceil_tf = best * 64 / 1e12
+                alt[other]["roofline_valu"]["measured_ceiling"] = {
+                    "TFLOPs": round(ceil_tf, 1), "frac": round(tf / ceil_tf, 4), "source": os.path.relpath(vp, ROOT)}
+        else:
+            g.close()
 
-    others = None
-    if world == 1 and args.other_configs:
-        # BASELINE configs[1] (c2, 512 x 512, N 4-32) and any others, same mode, same timing rule
-        others = {}
-        for name in filter(None, args.other_configs.split(",")):
-            if name == args.config or name not in CONFIGS:
-                continue
-            oNy, oNz, olo, ohi, odesc = CONFIGS[name]
-            h = dfamd.DigitalFilter(plane="synthetic", Ny=oNy, Nz=oNz, N_min=olo, N_max=ohi, seed=args.seed,
-                                    device=local_rank, coeff_mode=args.coeff_mode, rows_per_wave=args.rows_per_wave)
-            el3, p3 = timed(h)
-            ph = {"ypass": p3["ypass_ms"], "zpass": p3["zpass_ms"]}
-            d = max(ph, key=ph.get)
-            d_ms = ph[d] / max(1, p3["calls"])
-            d_ach = h.algorithmic_bytes(0 if d == "ypass" else 1) / (d_ms * 1e-3) / 1e9
-            others[name] = {"workload": odesc, "value": round(oNy * oNz * args.steps / el3, 1),
-                            "ms_per_step": round(el3 * 1e3 / args.steps, 4),
-                            "phase_ms_per_call": {k: round(p3[k] / max(1, p3["calls"]), 4)
-                                                  for k in ("rng_ms", "ypass_ms", "zpass_ms", "total_ms")},
-                            "roofline": ({"kernel": f"{d}_kernel", "achieved": round(d_ach, 1), "unit": "GB/s",
-                                          "frac": round(d_ach / HBM_PEAK_GBPS, 4)}
-                                         if args.coeff_mode == "packed" else None)}
-            h.close()
+    parity = None
+    if args.parity == "on":
+        pr = parity_check(dfamd, ctx, wl, args, f, calls_done, ref=ref_for_parity)
+        prs = ctx.gather(pr)
+        parity = {"ok": all(p["ok"] for p in prs), "reference": "whole plane, one GPU, table mode, same seed/calls",
+                  "calls_compared": calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
+    if ref_for_parity is not None:
+        ref_for_parity.close()
+    comm = f.comm_info() if ctx.world > 1 else None
+    f.close()
 
-    out = None
-    if rank == 0:
+    others = {}
+    for oname in filter(None, others_arg.split(",")):
+        if oname == name or oname not in CONFIGS:
+            continue
+        try:
+            owl = plan_workload(oname, ctx.world, args.scaling)
+        except ValueError:
+            continue
+        h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd))
+        orecs = ctx.gather(orec)
+        osum = summarize(ctx, owl, args, orecs)
+        op = None
+        if args.parity == "on":
+            ops = ctx.gather(parity_check(dfamd, ctx, owl, args, h, calls_done))
+            op = all(p["ok"] for p in ops)
+        h.close()
+        others[oname] = {"workload": owl["desc"], "Ny": owl["Ny"], "Nz": owl["Nz"], "scaling": owl["scaling"],
+                         "parity_ok": op, **osum}
+        if oname == "c5":
+            others[oname]["projected_10k_steps_s"] = round(osum["ms_per_step"] * 10.0, 2)
+
+    if ctx.rank == 0:
         cpu = cpu_par = None
-        if args.cpu_baseline == "auto" and world == 1:
+        if args.cpu_baseline == "auto" and ctx.world == 1 and wl["plane"] != "native":
             try:
-                cpu = cpu_baseline(args, Ny, N_min, N_max)
+                cpu = cpu_baseline(args, wl["Ny"], wl["N_min"], wl["N_max"])
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": str(e)}
             try:
-                cpu_par = cpu_baseline_parallel(args, Ny, N_min, N_max)
+                cpu_par = cpu_baseline_parallel(args, wl["Ny"], wl["N_min"], wl["N_max"])
             except Exception as e:
                 cpu_par = {"error": str(e)}
-        per_call = {k: round(prof[k] / max(1, prof["calls"]), 4) for k in ("rng_ms", "ypass_ms", "halo_ms",
-                                                                            "zpass_ms", "total_ms")}
+        ms = head["ms_per_step"]
+        call_bytes = sum(r["call_bytes"] for r in recs)  # SURVEY 8d algorithmic bytes of one call, all ranks
         out = {
             "metric": "inflow cells/sec (filter(dt) call) + achieved HBM GB/s, 1/2/4/8 GPU",
-            "value": round(value, 1),
+            "value": head["value"],
             "unit": "cells/s",
-            "n_gpus": world,
+            "n_gpus": ctx.world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
+            "ms_per_step": ms,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": wl["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY 8d plane; rows from files/RST.dat + line.dat; pcg32 seed %d)" % args.seed,
-            "config": {"workload": desc, "Ny": Ny, "Nz": Nz, "N_min": N_min, "N_max": N_max,
-                       "dt": args.dt, "coeff_mode": args.coeff_mode, "rows_per_wave": args.rows_per_wave,
-                       "parallelism": f"z-strips x{world}" if world > 1 else "single GPU"},
-            "achieved_call_GBps": round(call_alg / (ms_per_step * 1e-3) / 1e9 * world, 1),
-            "call_hbm_frac": round(call_alg * world / (ms_per_step * 1e-3) / 1e9 / (HBM_PEAK_GBPS * world), 4),
-            "phase_ms_per_call": per_call,
-            "roofline": roofline,
+            "config": {"workload": wl["desc"], "name": name, "Ny": wl["Ny"], "Nz": wl["Nz"], "N_min": wl["N_min"],
+                       "N_max": wl["N_max"], "dt": args.dt, "coeff_mode": args.coeff_mode,
+                       "rows_per_wave": args.rows_per_wave,
+                       "parallelism": f"z-strips x{ctx.world}" if ctx.world > 1 else "single GPU"},
+            "parity_ok": parity["ok"] if parity else None,
+            "rng_collective": "allgather" if (comm or {}).get("rng_collective") else "none",
+            "phase_ms_per_call": head["phase_ms_per_call"],
+            "roofline": head["roofline"],
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
             "alt_modes": alt,
-            "other_configs": others,
-            "setup_s": round(t_setup, 3),
+            "other_configs": others or None,
+            "parity": parity,
+            "setup_s": rec["setup_s"],
         }
+        out["achieved_call_GBps"] = round(call_bytes / (ms * 1e-3) / 1e9, 1)
+        out["call_hbm_frac"] = round(call_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBPS * ctx.world), 4)
+        if "multi_gpu" in head:
+            out["multi_gpu"] = head["multi_gpu"]
         print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    if world > 1 or args.alt_modes == "off":
-        f.close()
+    ctx.barrier()
+    if ctx.dist is not None:
+        ctx.dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -97,7 +97,10 @@ struct df_handle {
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
-    int rng_replicate = 0; // z-strips: every rank counts every attempt block (no RNG all-gather)
+    // z-strips: every rank counts every attempt block, so the halo send/recv is the call's only
+    // collective (SURVEY 8e option B, north star "single RCCL halo exchange"). 0 = split counting
+    // plus a per-call all-gather of counts and accept masks (option A), ordered after the halo.
+    int rng_replicate = 1;
     int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
@@ -129,6 +132,7 @@ struct df_handle {
     bool split_count = false;
     ncclComm_t rng_comm = nullptr;           // second communicator: the count all-gather runs on rng_stream
     hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
+    hipEvent_t ev_halo = nullptr;            // split counting: the halo of the call just enqueued is done
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
     long long gen_launched = 0; // generations enqueued (generation n reads state slot n%2, writes (n+1)%2)
     long long gen_used = 0;     // generations consumed by a visible step (ctor step 0, filter, stage API)
@@ -389,6 +393,10 @@ int launch_gen(df_handle *h)
         const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
         if (h->rng_comm) { // the RNG's one exchange: accept counts (block, wave) and masks
+            // Never concurrent with the halo send/recv of the other communicator: every rank issues
+            // the all-gather only after its own halo group of the call just enqueued has completed,
+            // so the two communicators' kernels run in the same order on every rank.
+            if (h->ev_halo) HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
             NCCL_OR(ncclGroupStart());
             NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
             NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
@@ -474,6 +482,7 @@ int halo_loopback(df_handle *h)
     HIP_OR(launch_halo_check(h->send_l, h->recv_l, h->halo_elems, h->halo_loopback == 2, h->err_dev + 2, h->stream),
            DF_EHIP);
     HIP_OR(launch_halo_check(h->send_r, h->recv_r, h->halo_elems, 0, h->err_dev + 2, h->stream), DF_EHIP);
+    if (h->ev_halo) HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -494,6 +503,7 @@ int phase_halo_rccl(df_handle *h)
         NCCL_OR(ncclRecv(h->recv_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, h->stream));
     }
     NCCL_OR(ncclGroupEnd());
+    if (h->ev_halo) HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
     return phase_halo_unpack(h);
 }
 
@@ -517,6 +527,7 @@ int phase_zpass(df_handle *h, bool corr, bool sra, double dt)
 int write_csv_if(df_handle *h)
 {
     if (h->csv_path.empty()) return DF_OK;
+    if (h->solo_strip) return fail(DF_EINVAL, "DFAMD_SOLO_STRIP handle: timing only, no CSV");
     const size_t n = (size_t)h->Ny * h->Nz_loc;
     std::vector<double> f[5];
     double *src[5] = {h->c[0].fluc, h->c[1].fluc, h->c[2].fluc, h->T, h->rho};
@@ -937,6 +948,8 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         std::memcpy(&id, cfg->comm_id, sizeof(id));
         NCCL_OR(ncclCommInitRank(&h->comm, h->world, id, h->rank));
         NCCL_OR(ncclCommSplit(h->comm, 0, h->rank, &h->rng_comm, nullptr)); // RNG all-gather, own stream
+        HIP_OR(hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), DF_EHIP);
+        HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
         h->split_count = !h->rng_replicate;
     }
     return DF_OK;
@@ -989,6 +1002,7 @@ void destroy(df_handle *h)
     if (h->rng_comm) ncclCommDestroy(h->rng_comm);
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->ev_counted) (void)hipEventDestroy(h->ev_counted);
+    if (h->ev_halo) (void)hipEventDestroy(h->ev_halo);
     for (auto &g : h->graph)
         if (g) (void)hipGraphExecDestroy(g);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
@@ -1145,6 +1159,18 @@ bool valid_dev(df_handle *h)
     if (!valid(h)) return false;
     if (h->device < 0) {
         g_err = "host-only handle (created with device = -1) has no GPU state";
+        return false;
+    }
+    return true;
+}
+
+// Handles whose results may be read. A DFAMD_SOLO_STRIP handle (tools/strip_timing.py: one rank of
+// a split plane timed alone, halo never exchanged) computes wrong fields by design.
+bool valid_out(df_handle *h)
+{
+    if (!valid_dev(h)) return false;
+    if (h->solo_strip) {
+        g_err = "DFAMD_SOLO_STRIP handle: timing only, its fields and stream state are not results";
         return false;
     }
     return true;
@@ -1310,7 +1336,7 @@ int df_get_rho_T_fluc(df_handle *h) { return stage_elementwise(h, 2, 0, 0.0); }
 
 int df_get_field(df_handle *h, int which, double *out)
 {
-    if (!valid_dev(h) || !out) return DF_EINVAL;
+    if (!valid_out(h) || !out) return DF_EINVAL;
     const double *src = df_device_field(h, which);
     if (!src) return DF_EINVAL;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
@@ -1335,7 +1361,7 @@ int df_set_field(df_handle *h, int which, const double *host_in)
 
 const double *df_device_field(df_handle *h, int which)
 {
-    if (!valid_dev(h)) return nullptr;
+    if (!valid_out(h)) return nullptr;
     switch (which) {
     case DF_U: case DF_V: case DF_W: return h->c[which].fluc;
     case DF_T: return h->T;
@@ -1446,7 +1472,7 @@ int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n)
 
 int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
 {
-    if (!valid_dev(h)) return DF_EINVAL;
+    if (!valid_out(h)) return DF_EINVAL;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     int rc = sync_all(h);
     if (rc) return rc;
@@ -1585,7 +1611,7 @@ void *df_stream(df_handle *h) { return valid_dev(h) ? (void *)h->stream : nullpt
 
 int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n)
 {
-    if (!valid_dev(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
+    if (!valid_out(h) || !out || comp < 0 || comp > 2 || dir < 0 || dir > 1) return fail(DF_EINVAL, "bad argument");
     const CompDev &d = h->c[comp];
     const int width = dir ? h->Nz_loc + 2 * d.Nzp : h->Nz_loc;
     const int rows = dir ? h->Ny : h->Ny + 2 * d.Nyp;
@@ -1623,6 +1649,26 @@ int df_comm_unique_id(void *out, size_t len)
     return DF_OK;
 }
 
+int df_comm_info(df_handle *h, df_comm_stats *out)
+{
+    if (!valid(h) || !out) return fail(DF_EINVAL, "bad argument");
+    *out = df_comm_stats{};
+    if (h->comm) {
+        NCCL_OR(ncclCommCount(h->comm, &out->rccl_ranks));
+        NCCL_OR(ncclCommUserRank(h->comm, &out->rccl_rank));
+    }
+    const bool split = h->world > 1 || h->halo_loopback;
+    out->halo_peers = h->world > 1 ? (h->rank > 0) + (h->rank < h->world - 1) : (h->halo_loopback ? 2 : 0);
+    out->halo_bytes_sent = split ? (long long)out->halo_peers * (long long)h->halo_elems * 8 : 0;
+    out->rng_collective = h->split_count && h->rng_comm ? 1 : 0;
+    const long long others = (long long)h->rng_chunk * (h->world - 1);
+    out->rng_bytes_received =
+        out->rng_collective ? others * (long long)(sizeof(int) + kWavesPerBlock * sizeof(int) + kRngThreads * sizeof(uint16_t)) : 0;
+    out->rng_blocks_counted = h->split_count ? h->rng_chunk : h->rng_blocks;
+    out->rng_blocks_total = h->rng_blocks;
+    return DF_OK;
+}
+
 int df_rms_reset(df_handle *h)
 {
     if (!valid_dev(h)) return DF_EINVAL;
@@ -1649,7 +1695,7 @@ int df_rms_add(df_handle *h)
 
 int df_rms_get(df_handle *h, int which, double *out)
 {
-    if (!valid_dev(h) || !out || which < DF_U || which > DF_RHO) return fail(DF_EINVAL, "bad argument");
+    if (!valid_out(h) || !out || which < DF_U || which > DF_RHO) return fail(DF_EINVAL, "bad argument");
     if (!h->rms_acc || h->rms_count == 0) return fail(DF_EINVAL, "no df_rms_add since df_rms_reset");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     const size_t n = (size_t)h->Ny * h->Nz_loc;

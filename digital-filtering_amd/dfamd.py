@@ -43,6 +43,15 @@ class _Cfg(C.Structure):
     ]
 
 
+class CommStats(C.Structure):
+    _fields_ = [("rccl_ranks", C.c_int), ("rccl_rank", C.c_int), ("halo_peers", C.c_int), ("rng_collective", C.c_int),
+                ("halo_bytes_sent", C.c_longlong), ("rng_bytes_received", C.c_longlong),
+                ("rng_blocks_counted", C.c_longlong), ("rng_blocks_total", C.c_longlong)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Profile(C.Structure):
     _fields_ = [("calls", C.c_longlong), ("rng_ms", C.c_double), ("ypass_ms", C.c_double),
                 ("halo_ms", C.c_double), ("zpass_ms", C.c_double), ("total_ms", C.c_double)]
@@ -107,6 +116,7 @@ def lib():
         "df_stream": (C.c_void_p, [H]),
         "df_algorithmic_bytes": (C.c_double, [H, C.c_int]),
         "df_comm_unique_id": (C.c_int, [C.c_void_p, C.c_size_t]),
+        "df_comm_info": (C.c_int, [H, C.POINTER(CommStats)]),
         "df_destroy": (None, [H]),
     }
     for name, (res, args) in sig.items():
@@ -363,6 +373,12 @@ class DigitalFilter:
         p = Profile()
         _check(lib().df_get_profile(self._h, C.byref(p)))
         return p.as_dict()
+
+    def comm_info(self):
+        """df_comm_info: RCCL ranks, halo and RNG-collective bytes of one df_filter."""
+        st = CommStats()
+        _check(lib().df_comm_info(self._h, C.byref(st)))
+        return st.as_dict()
 
     def algorithmic_bytes(self, kernel=-1):
         return lib().df_algorithmic_bytes(self._h, kernel)

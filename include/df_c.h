@@ -201,6 +201,22 @@ double df_algorithmic_bytes(df_handle *h, int kernel /* -1 whole call, 0 ypass, 
 
 int df_comm_unique_id(void *out, size_t len); /* RCCL unique id, len >= 128 */
 
+/* What one df_filter of a z-strip handle exchanges (bench and monitoring).
+ * rccl_ranks comes from ncclCommCount on the handle's communicator (0: no RCCL). With the
+ * default replicated counting the halo send/recv is the call's only collective
+ * (rng_collective 0); df_set_tuning(h, "rng_replicate", 0) switches to split counting plus one
+ * all-gather of block counts, wave counts and accept masks per call (rng_collective 1). */
+typedef struct df_comm_stats {
+    int rccl_ranks, rccl_rank;    /* ncclCommCount / ncclCommUserRank; 0, 0 without RCCL */
+    int halo_peers;               /* neighbours this strip exchanges z-halo columns with (0-2) */
+    int rng_collective;           /* 1: per-call RNG all-gather (split counting); 0: none */
+    long long halo_bytes_sent;    /* per df_filter, all three components */
+    long long rng_bytes_received; /* per df_filter, RNG all-gather (0 when replicated) */
+    long long rng_blocks_counted; /* attempt blocks of 4096 this rank tests per call (K1) */
+    long long rng_blocks_total;   /* attempt blocks of the whole plane's call */
+} df_comm_stats;
+int df_comm_info(df_handle *h, df_comm_stats *out);
+
 void df_destroy(df_handle *h);
 const char *df_last_error(void);
 int df_abi_version(void);

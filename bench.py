@@ -275,7 +275,7 @@ def compare(h, ref, z0, z1):
 
 
 def parity_check(dfamd, ctx, wl, args, h, calls, ref=None):
-    """This rank's strip after `calls` filter(dt) calls against the whole plane run unsplit in table mode
+    """This rank's strip after construction + `calls` filter(dt) calls against the whole plane run unsplit in table mode
     on this rank's own GPU (packed and table mode, any strip count: bit-identical by construction)."""
     own = ref is None
     if own:
@@ -384,7 +384,7 @@ def main(argv=None):
     f, rec = run_config(dfamd, ctx, wl, args, comm_id)
     recs = ctx.gather(rec)
     head = summarize(ctx, wl, args, recs)
-    calls_done = 1 + args.warmup + args.steps  # constructor step 0 + warmup + timed
+    calls_done = args.warmup + args.steps  # filter(dt) calls after the constructor's step 0
 
     alt = None
     ref_for_parity = None
@@ -442,13 +442,15 @@ def main(argv=None):
         h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd))
         orecs = ctx.gather(orec)
         osum = summarize(ctx, owl, args, orecs)
-        op = None
+        op = ops = None
         if args.parity == "on":
             ops = ctx.gather(parity_check(dfamd, ctx, owl, args, h, calls_done))
             op = all(p["ok"] for p in ops)
         h.close()
         others[oname] = {"workload": owl["desc"], "Ny": owl["Ny"], "Nz": owl["Nz"], "scaling": owl["scaling"],
                          "parity_ok": op, **osum}
+        if ops and not op:
+            others[oname]["parity"] = [p for p in ops if not p["ok"]]
         if oname == "c5":
             others[oname]["projected_10k_steps_s"] = round(osum["ms_per_step"] * 10.0, 2)
 

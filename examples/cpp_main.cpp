@@ -6,6 +6,8 @@
 //   cpp-test filter N dt          N x filter(dt), prints sum(u'^2)
 //   cpp-test synth Ny Nz Nmin Nmax seed steps [csv]   synthetic plane, writes u'/v'/w'/T'/rho' CSV
 //   cpp-test rms seed             native grid, seeded, get_rms() -> ../files/cpp_vel_fluc_rms.csv
+//   cpp-test writers seed dt steps out   native grid, steps x filter(dt), then write_tecplot(out) and
+//                                 plot_RST_lerp() -> ../files/myRST.csv, ../files/duanRST.csv
 #include "df.hpp"
 
 #include <cstdlib>
@@ -26,6 +28,17 @@ int main(int argc, char **argv)
         const int steps = std::atoi(argv[7]);
         for (int s = 0; s < steps; ++s) df.filter(1e-8);
         df.write_csv(argc > 8 ? argv[8] : "cpp_vel_fluc.csv");
+        return 0;
+    }
+
+    if (argc > 5 && std::string(argv[1]) == "writers") {
+        config.seed = std::strtoull(argv[2], nullptr, 10);
+        config.seed_from_random_device = false;
+        DIGITAL_FILTER df(config);
+        const int steps = std::atoi(argv[4]);
+        for (int s = 0; s < steps; ++s) df.filter(std::atof(argv[3]));
+        df.write_tecplot(argv[5]);
+        df.plot_RST_lerp();
         return 0;
     }
 

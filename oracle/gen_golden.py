@@ -176,10 +176,41 @@ def rms_fixture(name, seed, synth=None, sample_rows=None, csv_head=12):
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arr)
 
 
+def writers_fixture(name, seed=42, dt=1e-8, nsteps=2, every=997):
+    """The reference's file writers on its native grid (f4): the per-call CSV of filter()
+    (df.cpp:466-467, 764-803), write_tecplot (712-762) and plot_RST_lerp (677-706). The CSV and
+    Tecplot files (~20 MB each) are kept as header + line count + every `every`-th line + the
+    sha256 of the coordinate text; myRST.csv / duanRST.csv (a few hundred lines) whole."""
+    import hashlib
+    files = os.path.join(RUN_ROOT, "files")
+    with tempfile.TemporaryDirectory() as d:
+        run("writers", RUN_ROOT, seed, dt, nsteps, d)
+        tec = open(os.path.join(d, "tecplot.dat")).read().splitlines()
+    csv = open(os.path.join(files, "cpp_vel_fluc.csv")).read().splitlines()
+    meta = {"seed": seed, "dt": dt, "nsteps": nsteps, "every": every}
+    # Tecplot BLOCK: 3 header lines, (Ny+1)(Nz+1) z then y vertex values, then u, v, w per cell
+    nv = 511 * 401
+    coords = tec[3:3 + 2 * nv]
+    meta["tecplot"] = {"header": tec[:3], "n_lines": len(tec),
+                       "coord_sha256": hashlib.sha256("\n".join(coords).encode()).hexdigest(),
+                       "sample": {str(i): tec[i] for i in range(3, len(tec), every)}}
+    cz = [",".join(l.split(",")[:2]) for l in csv[1:]]
+    meta["csv"] = {"header": csv[0], "n_lines": len(csv),
+                   "coord_sha256": hashlib.sha256("\n".join(cz).encode()).hexdigest(),
+                   "sample": {str(i): csv[i] for i in range(1, len(csv), every)}}
+    json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=0)
+    for f in ("myRST.csv", "duanRST.csv"):
+        open(os.path.join(OUT, f"{name}_{f}"), "w").write(open(os.path.join(files, f)).read())
+
+
 def main():
     if not os.path.exists(HARN):
         sys.exit("reference not built: make -C oracle/ref")
     os.makedirs(OUT, exist_ok=True)
+    if len(sys.argv) > 1:  # regenerate named fixtures only, e.g. `gen_golden.py writers`
+        for name in sys.argv[1:]:
+            {"writers": lambda: writers_fixture("writers_native_s42")}[name]()
+        return
     kat()
     rng_fixture(42)
     rng_fixture(1234)
@@ -195,6 +226,8 @@ def main():
     grid_fixture("grid_s3", 3, 60, 200, 1e-8, 2, full_steps=(0, 2))
     # the reference driver's get_rms() (500 steps at dt = 1e-5) on its native grid
     rms_fixture("rms_native_s42", 42)
+    # the reference's file writers on its native grid: per-call CSV, write_tecplot, plot_RST_lerp
+    writers_fixture("writers_native_s42")
     manifest = {
         "generator": "oracle/gen_golden.py",
         "reference": "connorswitala/digital-filtering @ /root/reference (df.cpp compiled unmodified, "

@@ -278,6 +278,19 @@ int main(int argc, char **argv)
         for (int s = 1; s <= nsteps; ++s) { df.filter(dt); dump_state(df, out, "step" + std::to_string(s)); }
         return 0;
     }
+    if (mode == "writers") { // writers <root> <seed> <dt> <nsteps> <outdir>: the reference's file outputs
+        // filter() writes ../files/cpp_vel_fluc.csv after every call (df.cpp:466-467); then
+        // write_tecplot (df.cpp:712-762) and plot_RST_lerp (677-706, ../files/myRST.csv, duanRST.csv).
+        double dt = strtod(argv[4], 0);
+        int nsteps = atoi(argv[5]);
+        std::string out = argv[6];
+        DIGITAL_FILTER df(cfg);
+        for (int s = 1; s <= nsteps; ++s) df.filter(dt);
+        df.write_tecplot(out + "/tecplot.dat");
+        df.plot_RST_lerp();
+        dump_state(df, out, "final");
+        return 0;
+    }
     if (mode == "rms") { // rms <root> <seed> <outdir> [Ny Nz Nmin Nmax]: the reference driver's call (cpp-main.cpp:12-17)
         std::string out = argv[4];
         DIGITAL_FILTER df(cfg);

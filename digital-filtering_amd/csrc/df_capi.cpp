@@ -694,10 +694,9 @@ int plan_rng(df_handle *h)
         // ceil(2^64 / W): floor(p * inv / 2^64) == p / W for every p < 2^32
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
+    g.gen_compact = 1;
+    if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
     g.nt_stores = 1; // noise written past the caches: it is read once, by the next call's sweeps (A/B -1.4%)
-    const PcgJump hop = pcg_jump(4ull * (64 - 1)); // after an attempt's 4 draws -> the lane's next attempt
-    g.hop_mult = hop.mult;
-    g.hop_plus = hop.plus;
     const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
     g.next_mult = next.mult;
     g.next_plus = next.plus;
@@ -1538,6 +1537,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->halo_loopback = value;
     }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
+    else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "graph") h->use_graph = value != 0;
     else if (k == "ywin_T" || k == "zwin_T") {
         if (value < 0 || value > (1 << 24) || (value & (value - 1)))

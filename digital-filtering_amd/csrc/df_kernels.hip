@@ -127,15 +127,24 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
         return;
     }
     uint64_t st = thread_first_state(g, sin->state, gb, tid);
-    int cnt = 0;
-    uint32_t bits = 0;
+    const uint64_t st0 = st;
+    uint32_t bits = 0, unsure = 0;
 #pragma unroll 4
     for (int m = 0; m < kRngPerThread; ++m) {
-        const bool acc = polar_accept(st);
-        cnt += acc ? 1 : 0;
-        bits |= (acc ? 1u : 0u) << m;
-        st = g.hop_mult * st + g.hop_plus;
+        const int v = polar_screen(st); // st stays at the attempt's start
+        bits |= (v > 0 ? 1u : 0u) << m;
+        unsure |= (v < 0 ? 1u : 0u) << m;
+        st = g.next_mult * st + g.next_plus; // the lane's next attempt, 64 attempts on
     }
+    // ~2e-5 of the attempts: the exact double test of polar_attempt (random.tcc:1822-1826)
+    while (unsure) {
+        const int m = __builtin_ctz(unsure);
+        unsure &= unsure - 1;
+        uint64_t s = st0;
+        for (int k = 0; k < m; ++k) s = g.next_mult * s + g.next_plus;
+        if (polar_attempt(s).accept) bits |= 1u << m;
+    }
+    int cnt = __builtin_popcount(bits);
     masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
     if ((tid & 63) == 0) {
@@ -490,6 +499,150 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     }
 }
 
+// K3, compacted form (the default; RngGeom::gen_compact). The sequential form above runs the
+// transform (4 draws, log, sqrt, divide) in every iteration with the ~21% rejected lanes idle, and
+// walks the stream position per iteration in scalar code. Here a wave first appends the state of each
+// accepted attempt to a wave-private LDS ring, in rank order (slot k = the wave's k-th accepted attempt,
+// stream positions q0 + 2k and q0 + 2k + 1), and every 4 iterations turns each full run of 64 slots into
+// one batch with all 64 lanes busy. A batch covers 128 consecutive stream positions, so whether it stores
+// anything on this GPU is one scalar range test; the r_zs interior (df.cpp:377) and other strips' columns
+// are skipped a batch at a time. Same draws, same arithmetic, same destinations: bit-identical.
+constexpr int kGenRing = 512; // slots per wave: < 64 carried + 4 iterations x 64 appended between flushes
+
+__device__ __forceinline__ void gen_batch(const RngGeom &g, const uint64_t *ring, int head, int n, long long rank0,
+                                          uint64_t f, long long A, RngStateDev *__restrict__ sout, int lane)
+{
+    const long long rk = rank0 + head; // rank of the batch's first slot (uniform)
+    if (rk >= A) return;               // past the call's last attempt
+    const uint64_t qf = f + 2ull * (uint64_t)rk;
+    const StreamPos P0 = stream_pos(g, qf);
+    const int su = uniform(P0.sidx < 6 ? P0.sidx : 5);
+    const uint32_t left = (g.rows[su] - P0.row) * g.width[su] - P0.col;
+    const bool fast = P0.sidx < 6 && g.width[su] >= 2 * 64 && 2u * (uint32_t)n <= left;
+    const bool holds_last = rk <= A - 1 && A - 1 < rk + n;
+    if (fast && !holds_last) { // whole-batch skip: one row of one array, no column stored here
+        const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n, W = g.width[su];
+        if (c1 <= W) {
+            bool idle;
+            if (su & 1) {
+                const uint32_t nzp = (uint32_t)g.Nzp[su >> 1];
+                idle = (!g.is_first || c0 >= nzp) && (!g.is_last || c1 <= nzp + (uint32_t)g.Nz_g);
+            } else {
+                idle = c1 <= (uint32_t)g.z0 || c0 >= (uint32_t)g.z1;
+            }
+            if (idle) return;
+        }
+    }
+    if (lane >= n) return;
+    const long long rank = rk + lane;
+    if (rank >= A) return;
+    const uint64_t st = ring[(head + lane) & (kGenRing - 1)];
+    const uint64_t q0 = qf + 2ull * (uint64_t)lane;
+    double *d0, *d1;
+    if (fast) { // one array, at most one row wrap: uniform array index, scalar tables
+        const uint32_t W = g.width[su];
+        StreamPos p0 = {su, P0.row, P0.col + 2u * (uint32_t)lane};
+        if (p0.col >= W) {
+            p0.col -= W;
+            p0.row++;
+        }
+        StreamPos p1 = {su, p0.row, p0.col + 1u};
+        if (p1.col == W) {
+            p1.col = 0;
+            p1.row++;
+        }
+        d0 = stream_dest(g, p0);
+        d1 = stream_dest(g, p1);
+    } else {
+        const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
+        d0 = stream_dest(g, p0);
+        d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
+    }
+    const bool last = rank == A - 1;
+    if (!(d0 || d1 || last)) return;
+    uint64_t s4 = st;
+    PolarAttempt a;
+    if (g.debug_flags & 4) {
+        a.x = (double)(uint32_t)st * 1e-10;
+        a.y = 0.5;
+        a.r2 = 0.5;
+        s4 = st + 4;
+    } else {
+        a = polar_attempt(s4); // the draws K1 tested
+    }
+    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * log(a.r2) / a.r2);
+    const double xm = a.x * mult;
+    const double ym = a.y * mult;
+    const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;
+    if (g.debug_flags & 2) {
+        if (n0 == 1234.5) *d0 = n1; // keep the values alive
+    } else if (d0 && d1 == d0 + 1 && ((uintptr_t)d0 & 15) == 0) {
+        if (g.nt_stores) __builtin_nontemporal_store(dvec2{n0, n1}, reinterpret_cast<dvec2 *>(d0));
+        else *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
+    } else {
+        if (d0) *d0 = n0;
+        if (d1) *d1 = n1;
+    }
+    if (last) {
+        sout->state = s4; // state after this attempt's 4th output
+        sout->saved_flag = (int)((g.Q - f) & 1u);
+        sout->saved = xm;
+    }
+}
+
+__global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGeom g,
+                                                                          const RngStateDev *__restrict__ sin,
+                                                                          RngStateDev *__restrict__ sout,
+                                                                          const WaveTask *__restrict__ tasks,
+                                                                          const int *__restrict__ ntasks,
+                                                                          const uint16_t *__restrict__ masks)
+{
+    __shared__ uint64_t ring_all[kRngThreads / 64][kGenRing];
+    const int lane = threadIdx.x & 63;
+    uint64_t *ring = ring_all[threadIdx.x >> 6];
+    const int split = g.gen_split;
+    const int vslot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    const int slot = vslot / split, sub = vslot - slot * split;
+    if (slot >= *ntasks) return;
+    const int gw = uniform(tasks[slot].gw);
+    long long rank_w = tasks[slot].r_lo; // uniform
+    const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
+    const uint32_t bits = masks[(size_t)b * kRngThreads + tid];
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    uint64_t st = thread_first_state(g, sin->state, b, tid);
+    const int per = kRngPerThread / split, m0 = sub * per, m1 = m0 + per;
+    for (int m = 0; m < m0; ++m) {
+        st = g.next_mult * st + g.next_plus;
+        rank_w += __popcll(__ballot((bits >> m) & 1u));
+    }
+    const long long rank0 = rank_w; // rank of ring slot 0
+    int tail = 0, head = 0;         // uniform
+    for (int m = m0; m < m1; ++m) {
+        const bool acc = (bits >> m) & 1u;
+        const uint64_t mask = __ballot(acc);
+        if (acc) {
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            ring[(tail + below) & (kGenRing - 1)] = st;
+        }
+        tail += __popcll(mask);
+        st = g.next_mult * st + g.next_plus;
+        const bool fin = m == m1 - 1;
+        if (fin || ((m - m0) & 3) == 3) {
+            // the ring is wave-private and LDS ops of one wave complete in order: only the compiler
+            // must not move the reads above the appends
+            __asm__ volatile("" ::: "memory");
+            while (tail - head >= 64 || (fin && tail > head)) {
+                const int n = min(64, tail - head);
+                gen_batch(g, ring, head, n, rank0, f, A, sout, lane);
+                head += n;
+            }
+            __asm__ volatile("" ::: "memory");
+        }
+    }
+}
+
 // K2 + K2c in one block for planes of at most 1024 attempt blocks (c1, c2, the reference's own
 // grid): the scan of the block counts (one count per thread), the attempt-shortage check and the
 // wave plan, with the offsets kept in LDS. One launch instead of three: small planes are bound by
@@ -589,8 +742,12 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part,
                            wave_counts, nb_total, tasks, ntasks);
     }
-    hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in, st_out,
-                       tasks, ntasks, masks);
+    if (g.gen_compact)
+        hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g,
+                           st_in, st_out, tasks, ntasks, masks);
+    else
+        hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in,
+                           st_out, tasks, ntasks, masks);
     return hipGetLastError();
 }
 

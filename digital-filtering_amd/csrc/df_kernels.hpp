@@ -49,7 +49,6 @@ struct WaveTask {
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
-    uint64_t hop_mult, hop_plus;   // jump over 63*4 outputs (after an attempt's 4 draws to the lane's next)
     uint64_t next_mult, next_plus; // jump over 64*4 outputs (attempt start to the lane's next one)
     const PcgJumpDev *jump_block;  // [nblocks]: jump over 4*4096*b outputs
     const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*(1024*(tid/64) + tid%64) outputs
@@ -59,6 +58,7 @@ struct RngGeom {
     int nt_stores;                 // noise pairs stored non-temporally
     int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
                                    // iterations, so few-wave planes get short serial chains
+    int gen_compact;               // K3 form: 1 = accepted attempts compacted into full batches (default), 0 = sequential
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];

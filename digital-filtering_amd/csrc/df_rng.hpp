@@ -95,27 +95,28 @@ DF_HD PolarAttempt polar_attempt(uint64_t &state)
     return a;
 }
 
-// The accept decision of polar_attempt alone (K1). A float screen from the high words decides
-// all but the attempts within 1e-5 of the unit circle or of the origin, which take the exact
-// double test: |xf - x| <= 2^-24*2 (fl(hi)) + 2^-24 (subtract) + 2^-31 (dropped lo) < 1.9e-7, so
+// Two pcg32 steps at once: state -> mult2*state + inc2 (pcg_jump(2)).
+constexpr uint64_t kPcgMult2 = 0x685f98a2018fade9ULL;
+constexpr uint64_t kPcgInc2 = 0x1a08ee1184ba6d32ULL;
+
+// K1's accept decision, screened in float from the high words; it decides all but the attempts within
+// 1e-5 of the unit circle or of the origin, which take the exact double test:
+// |xf - x| <= 2^-24*2 (fl(hi)) + 2^-24 (subtract) + 2^-31 (dropped lo) < 1.9e-7, so
 // |r2f - r2| < 2*2*1.9e-7 + 3 float roundings of values <= 2 < 1.2e-6.
-DF_HD bool polar_accept(uint64_t &state)
+// Computed from the attempt's first state s0, without stepping it: it needs
+// only the high words o[1] = output(s1) and o[3] = output(s3), i.e. two 64-bit multiply-adds (s1 = one
+// step, s3 = two more) and two outputs instead of four of each. Returns 1 (accept), 0 (reject) or -1
+// (within 1e-5 of the circle or the origin: the caller redoes the exact double test, polar_attempt).
+DF_HD int polar_screen(uint64_t s0)
 {
-    uint32_t o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        o[i] = pcg_output(state);
-        state = state * kPcgMult + kPcgInc;
-    }
-    const float xf = (float)o[1] * 4.656612873077392578125e-10f - 1.0f; // 2^-31
-    const float yf = (float)o[3] * 4.656612873077392578125e-10f - 1.0f;
+    const uint64_t s1 = s0 * kPcgMult + kPcgInc;
+    const uint64_t s3 = s1 * kPcgMult2 + kPcgInc2;
+    const float xf = (float)pcg_output(s1) * 4.656612873077392578125e-10f - 1.0f; // 2^-31
+    const float yf = (float)pcg_output(s3) * 4.656612873077392578125e-10f - 1.0f;
     const float r2f = xf * xf + yf * yf;
-    if (r2f > 1e-5f && r2f < 1.0f - 1e-5f) return true;
-    if (r2f > 1.0f + 1e-5f) return false;
-    const double x = 2.0 * canonical_from(o[0], o[1]) - 1.0;
-    const double y = 2.0 * canonical_from(o[2], o[3]) - 1.0;
-    const double r2 = x * x + y * y;
-    return !(r2 > 1.0 || r2 == 0.0);
+    if (r2f > 1e-5f && r2f < 1.0f - 1e-5f) return 1;
+    if (r2f > 1.0f + 1e-5f) return 0;
+    return -1;
 }
 
 } // namespace dfamd

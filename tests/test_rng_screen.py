@@ -1,5 +1,5 @@
 """K1's accept test screens attempts in float and falls back to the exact double test near the
-unit circle (df_rng.hpp polar_accept). On the host, with the product header itself, it must take
+unit circle (df_rng.hpp polar_screen). On the host, with the product header itself, it must take
 the same decision as the exact test for every attempt (2e7 per seed; ~600 land in the band)."""
 import os
 import shutil

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -1187,6 +1189,17 @@ const char *df_last_error(void) { return g_err.c_str(); }
 
 size_t df_config_sizeof(void) { return sizeof(df_config_c); }
 
+const char *df_data_dir(void)
+{
+    static const std::string dir = [] {
+        Dl_info info{};
+        std::string lib = dladdr((void *)&df_data_dir, &info) && info.dli_fname ? info.dli_fname : "";
+        const size_t slash = lib.find_last_of('/');
+        return (slash == std::string::npos ? std::string(".") : lib.substr(0, slash)) + "/data";
+    }();
+    return dir.c_str();
+}
+
 void df_config_default(df_config_c *cfg)
 {
     std::memset(cfg, 0, sizeof(*cfg));
@@ -1198,7 +1211,11 @@ void df_config_default(df_config_c *cfg)
     cfg->seed = 0;
     cfg->seed_from_random_device = 1;
     cfg->plane = DF_PLANE_NATIVE;
-    cfg->coeff_mode = DF_COEFF_PACKED;
+    cfg->coeff_mode = DF_COEFF_TABLE; // same fields bit for bit as DF_COEFF_PACKED, no B stream
+    static const std::string rst = std::string(df_data_dir()) + "/RST.dat";
+    static const std::string line = std::string(df_data_dir()) + "/line.dat";
+    cfg->vel_fluc_file = rst.c_str();
+    cfg->line_file = line.c_str();
     cfg->world = 1;
     cfg->rows_per_wave = 0;
 }

@@ -76,6 +76,7 @@ def lib():
         "df_abi_version": (C.c_int, []),
         "df_last_error": (C.c_char_p, []),
         "df_config_default": (None, [C.POINTER(_Cfg)]),
+        "df_data_dir": (C.c_char_p, []),
         "df_create": (H, [C.POINTER(_Cfg)]),
         "df_create_group": (C.c_int, [C.POINTER(_Cfg), C.c_int, C.POINTER(H)]),
         "df_filter": (C.c_int, [H, C.c_double]),

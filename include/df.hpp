@@ -41,8 +41,12 @@ using namespace std; // as the reference header does (df.hpp:18)
 constexpr double pi_c = -2.0 * 3.14159265358979323846;             // df.hpp:16
 typedef std::vector<double> Vector;                                 // df.hpp:19
 
-#ifndef DF_DATA_DIR
-#define DF_DATA_DIR "digital-filtering_amd/data"
+// Input profiles: DF_DATA_DIR if the build defines it, else the data/ directory installed next to
+// libdfamd.so (df_data_dir(); independent of the working directory).
+#ifdef DF_DATA_DIR
+inline std::string df_default_data_dir() { return DF_DATA_DIR; }
+#else
+inline std::string df_default_data_dir() { return df_data_dir(); }
 #endif
 
 struct FilterField { // df.hpp:24-34
@@ -66,15 +70,17 @@ struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     double d_i = 0.0013, rho_e = 0.044, U_e = 869.1, mu_e = 7.1212e-6;
     int vel_file_offset = 0, vel_file_N_values = 0;
     std::string grid_file;                                   // DF_PLANE_GRID: Tecplot BLOCK grid (write_tecplot layout)
-    std::string vel_fluc_file = DF_DATA_DIR "/RST.dat";      // RST profile (reference: ../files/RST.dat)
+    std::string vel_fluc_file = df_default_data_dir() + "/RST.dat"; // RST profile (reference: ../files/RST.dat)
     // ---- extensions
-    std::string line_file = DF_DATA_DIR "/line.dat";         // mean profile (reference: ../line.dat)
+    std::string line_file = df_default_data_dir() + "/line.dat";    // mean profile (reference: ../line.dat)
     std::uint64_t seed = 0;
     bool seed_from_random_device = true;                     // df.cpp:334
     int plane = DF_PLANE_NATIVE;                             // DF_PLANE_SYNTHETIC: Ny x Nz, N in [N_min, N_max]
     int Ny = 0, Nz = 0, N_min = 0, N_max = 0;                // DF_PLANE_GRID: Ny x Nz cells of grid_y/grid_z
     Vector grid_y, grid_z;                                   // DF_PLANE_GRID vertices, (Ny+1)*(Nz+1), j*(Nz+1)+k
-    int coeff_mode = DF_COEFF_PACKED;
+    // Drop-in default: the per-N table (bit-identical fields, ~8x faster at c3, no 20-85 GB
+    // coefficient stream beside the solver); DF_COEFF_PACKED streams the reference's by/bz.
+    int coeff_mode = DF_COEFF_TABLE;
     std::string csv_path;                                    // e.g. "../files/cpp_vel_fluc.csv" (df.cpp:466)
     std::string rms_csv_path = "../files/cpp_vel_fluc_rms.csv"; // df.cpp:623
     int device = 0;

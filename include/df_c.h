@@ -98,7 +98,12 @@ typedef struct df_profile {
     double total_ms;      /* first event to last event of each call, summed */
 } df_profile;
 
+/* Reference defaults (df.cpp:7-16) plus: coeff_mode DF_COEFF_TABLE (bit-identical to
+ * DF_COEFF_PACKED, no coefficient stream), vel_fluc_file / line_file = the profiles in
+ * df_data_dir(). */
 void df_config_default(df_config_c *cfg);
+/* The data/ directory next to the loaded libdfamd.so (RST.dat, line.dat). */
+const char *df_data_dir(void);
 
 /* DIGITAL_FILTER::DIGITAL_FILTER(DFConfig) (df.hpp:89, df.cpp:4-66): setup plus
  * the constructor's step 0 (noise, sweeps, RST scaling; no correlation, no SRA).

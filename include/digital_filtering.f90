@@ -206,7 +206,7 @@ module DIGITAL_FILTERING
         ! DF_PLANE_GRID: the inflow grid's vertices, (Ny+1)*(Nz+1) each, index j*(Nz+1)+k+1
         ! (Ny x Nz cells, row 1 at the wall); unallocated -> grid_file (Tecplot BLOCK, write_tecplot layout)
         real(kind=dp), allocatable :: grid_y(:), grid_z(:)
-        integer :: coeff_mode = 0                    ! DF_COEFF_PACKED / DF_COEFF_TABLE
+        integer :: coeff_mode = 1                    ! DF_COEFF_TABLE (default: same fields, no B stream) / DF_COEFF_PACKED
         character(len=256) :: csv_file = ''          ! non-blank: reference CSV after every filter
         integer :: device = 0                        ! HIP device; -1 = host-only handle (setup queries)
         logical :: host_mirror = .true.              ! refresh DF%u%fluc ... after every filter
@@ -276,8 +276,8 @@ contains
             return
         end if
         call get_environment_variable('DF_DATA_DIR', dir, n, st)
-        if (st /= 0 .or. n == 0) dir = 'digital-filtering_amd/data'
-        path = trim(dir) // '/' // name
+        path = ''  ! blank: keep df_config_default's path (df_data_dir(), next to libdfamd.so)
+        if (st == 0 .and. n > 0) path = trim(dir) // '/' // name
     end function data_path
 
     ! DIGITAL_FILTER(DFConfig) (df.f90:74-138 shape; df.cpp:4-66 semantics): setup and
@@ -303,8 +303,10 @@ contains
         c%vel_file_offset = config%vel_file_offset
         c%vel_file_N_values = config%vel_file_N_values
         call c_string(config%grid_file, s_grid, c%grid_file)
-        call c_string(data_path(config%vel_fluc_file, 'RST.dat'), s_rst, c%vel_fluc_file)
-        call c_string(data_path(config%line_file, 'line.dat'), s_line, c%line_file)
+        if (len_trim(data_path(config%vel_fluc_file, 'RST.dat')) > 0) &
+            call c_string(data_path(config%vel_fluc_file, 'RST.dat'), s_rst, c%vel_fluc_file)
+        if (len_trim(data_path(config%line_file, 'line.dat')) > 0) &
+            call c_string(data_path(config%line_file, 'line.dat'), s_line, c%line_file)
         call c_string(config%csv_file, s_csv, c%csv_path)
         if (config%seed >= 0) then
             c%seed = config%seed

@@ -159,6 +159,25 @@ def test_reference_defaults_in_config():
     # df.cpp:7-10 hard-coded values
     assert (cfg.d_i, cfg.rho_e, cfg.U_e, cfg.mu_e) == (0.0013, 0.044, 869.1, 7.1212e-6)
     assert cfg.seed_from_random_device == 1 and cfg.plane == 0 and cfg.world == 1
+    # drop-in extensions: table mode (bit-identical to packed) and the profiles next to the library
+    assert cfg.coeff_mode == dfamd.COEFF["table"]
+    dfamd.lib().df_data_dir.restype = C.c_char_p
+    data = dfamd.lib().df_data_dir().decode()
+    assert os.path.samefile(data, dfamd.DATA)
+    assert cfg.vel_fluc_file.decode() == data + "/RST.dat" and cfg.line_file.decode() == data + "/line.dat"
+
+
+def test_default_config_creates_the_native_plane():
+    # an untouched df_config_c (no paths set by the caller) finds its input profiles by itself
+    import ctypes as C
+    cfg = dfamd._Cfg()
+    dfamd.lib().df_config_default(C.byref(cfg))
+    cfg.device = -1
+    h = dfamd.lib().df_create(C.byref(cfg))
+    assert h, dfamd.lib().df_last_error().decode()
+    f = dfamd.DigitalFilter(_handle=h)
+    assert (f.Ny, f.Nz) == (510, 400)
+    f.close()
 
 
 def test_d_i_from_config_changes_the_setup():

@@ -99,6 +99,7 @@ struct df_handle {
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
+    int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     // z-strips: every rank counts every attempt block, so the halo send/recv is the call's only
     // collective (SURVEY 8e option B, north star "single RCCL halo exchange"). 0 = split counting
     // plus a per-call all-gather of counts and accept masks (option A), ordered after the halo.
@@ -220,6 +221,7 @@ SweepArgs sweep_args(df_handle *h)
     a.heavy_first = h->heavy_first;
     a.yunroll = h->yunroll;
     a.ywindow = h->ywindow;
+    a.ycoop = h->ycoop;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
     a.ynt_stores = h->ynt_stores;
@@ -1541,6 +1543,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "ycoop") h->ycoop = value != 0;
     else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter
         if (h->group) return fail(DF_EINVAL, "rng_replicate applies to RCCL or single handles, not in-process groups");
         h->rng_replicate = value != 0;

@@ -1030,6 +1030,65 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
     }
 }
 
+// K4, block-cooperative form for long tap chains (packed mode; SweepArgs::ycoop). One BLOCK per
+// (strip, row) tile instead of one wave: the tile's 2N+1 taps go in chunks of 4*KPW; wave w loads taps
+// w, w+4, ... of the chunk (KPW coefficient and noise pairs in flight per wave, 4*KPW per tile), writes
+// the products b*n to LDS, and after a barrier thread k < 128 adds cell k's products in tap order.
+// Every product and every addition is the one the per-wave kernel performs, in the same order
+// i = -N..N: bit-identical. On the reference's own grid (N_y up to 212, ~6 tiles per SIMD) a wave's
+// serial chain of 2N+1 dependent load rounds, not HBM bandwidth, set the per-wave kernel's time.
+template <bool NT, int KPW>
+__global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
+{
+    constexpr int CH = 4 * KPW; // taps per chunk
+    __shared__ double2 prod[CH][kStrip / 2];
+    const int c = blockIdx.y;
+    if (!((a.comps_mask >> c) & 1)) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int Ny = a.Ny;
+    const int per_xcd = gridDim.x >> 3; // XCD-aware order, as ypass_kernel
+    const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= a.nstrips * Ny) return; // block-uniform
+    const int s = tile / Ny;
+    int j = tile - s * Ny;
+    if (a.heavy_first) j = Ny - 1 - j;
+    const int N = a.Ny_st[c][(size_t)s * Ny + j];
+    const int T = 2 * N + 1;
+    const int col = s * kStrip + 2 * lane;
+    const bool live = col < a.Nz_loc;
+    const double *bp = a.By[c] + a.byoff[c][(size_t)s * Ny + j] + 2 * lane;       // tap t at bp + t*128
+    const double *np = a.ry[c] + (size_t)(j + a.Nyp[c] - N) * a.Pz + col;          // tap t at np + t*Pz
+    double acc = 0.0; // thread k < 128: cell s*128 + k
+    for (int t0 = 0; t0 < T; t0 += CH) {
+        double2 b[KPW], n[KPW];
+#pragma unroll
+        for (int k = 0; k < KPW; ++k) {
+            const int t = t0 + w + 4 * k;
+            if (live && t < T) {
+                b[k] = ldB<NT>(bp + (ptrdiff_t)t * kStrip);
+                n[k] = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * a.Pz), t);
+            } else {
+                b[k] = n[k] = make_double2(0.0, 0.0);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KPW; ++k) prod[w + 4 * k][lane] = make_double2(b[k].x * n[k].x, b[k].y * n[k].y);
+        __syncthreads();
+        if (threadIdx.x < kStrip) {
+            const double *pc = reinterpret_cast<const double *>(&prod[0][0]) + threadIdx.x;
+            const int nt = min(CH, T - t0);
+            for (int u = 0; u < nt; ++u) acc += pc[u * kStrip];
+        }
+        __syncthreads();
+    }
+    const int k = s * kStrip + (int)threadIdx.x;
+    if (threadIdx.x < kStrip && k < a.Nz_loc) {
+        double *o = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + k;
+        if (a.ynt_stores) __builtin_nontemporal_store(acc, o);
+        else *o = acc;
+    }
+}
+
 template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
 {
     const int nrowblk = (a.Ny + R - 1) / R;
@@ -1058,6 +1117,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
+    if (!table && a.ycoop) {
+        const long long tiles = (long long)a.nstrips * a.Ny;
+        const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);
+        if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 16>), grid, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((ypass_coop_kernel<false, 16>), grid, dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     switch (rows_per_wave) {
     case 1: return table ? launch_ypass_t<1, true>(a, st) : launch_ypass_t<1, false>(a, st);
     case 2: return table ? launch_ypass_t<2, true>(a, st) : launch_ypass_t<2, false>(a, st);

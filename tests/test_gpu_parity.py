@@ -131,8 +131,9 @@ def test_golden_synthetic(name):
     check_golden_case(name)
 
 
-@pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8)),
-                                         ("table", dict(yunroll=8))])
+@pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8, ycoop=0)),
+                                         ("packed", dict(ycoop=1)), ("table", dict(yunroll=8)),
+                                         ("table", dict(gen_compact=0))])
 def test_golden_native_grid(mode, tuning):
     # the reference's own grid (N_y up to 212): default shapes and the deep y-pass pipeline
     g = np.load(os.path.join(GOLDEN, "native_s42.npz"))
@@ -216,7 +217,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8), dict(rows_per_wave=4, yunroll=8, nt_loads=0),
                 dict(rows_per_wave=2, yunroll=8, nt_loads=1), dict(gen_split=1), dict(gen_split=4),
                 dict(gen_split=16), dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256),
-                dict(ywin_T=0, zwin_T=4096, zwin_W=0)]
+                dict(ywin_T=0, zwin_T=4096, zwin_W=0), dict(ycoop=1), dict(gen_compact=0, ycoop=0),
+                dict(gen_compact=1, gen_split=2)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -419,14 +421,17 @@ def _grid_case(name="grid_s3"):
     return np.load(os.path.join(GOLDEN, name + ".npz"))
 
 
-@pytest.mark.parametrize("mode,rpw", [("packed", 0), ("packed", 1), ("packed", 8), ("table", 0), ("table", 2)])
-def test_golden_grid_plane_per_cell_halfwidths(mode, rpw):
+@pytest.mark.parametrize("mode,rpw,tuning", [("packed", 0, {}), ("packed", 1, {}), ("packed", 8, {}),
+                                             ("packed", 0, dict(ycoop=1)), ("table", 0, {}), ("table", 2, {})])
+def test_golden_grid_plane_per_cell_halfwidths(mode, rpw, tuning):
     """Per-cell N (the reference's calculate_filter_properties on a real grid) vs the
     reference's own fields (tests/golden/grid_s3, gen_golden.grid_fixture)."""
     g = _grid_case()
     st = (int(g["start_state"]), int(g["start_saved_flag"]), float(g["start_saved"]))
     f = dfamd.DigitalFilter(plane="grid", grid_y=g["grid_y"], grid_z=g["grid_z"], device=0, resume=st,
                             coeff_mode=mode, rows_per_wave=rpw)
+    for k, v in tuning.items():
+        f.set_tuning(k, v)
     assert f.plane_info() == (2, True)
     o = O.Filter(plane=O.PLANE_GRID, Ny=int(g["Ny_in"]), Nz=int(g["Nz_in"]), grid_y=g["grid_y"],
                  grid_z=g["grid_z"], rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))

@@ -634,7 +634,11 @@ int plan_strips(df_handle *h)
             h->rows_per_wave = 1;
             if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
         } else h->rows_per_wave = 2;
+        // Long chains, packed: one block per tile, 8 taps per wave per chunk (the reference's grid: y-pass
+        // 0.209 -> 0.181 ms, call -9%; profiles/r2/ab_ycoop_native.jsonl). c3-class planes lose with it.
+        if (h->coeff_mode == DF_COEFF_PACKED && long_chain) h->ycoop = 2;
     }
+    if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -1543,7 +1547,11 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
-    else if (k == "ycoop") h->ycoop = value != 0;
+    else if (k == "ycoop") {
+        if (value < 0 || value > 3)
+            return fail(DF_EINVAL, "ycoop must be 0 or 1, 2, 3 (16, 8, 4 taps per wave per chunk)");
+        h->ycoop = value;
+    }
     else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter
         if (h->group) return fail(DF_EINVAL, "rng_replicate applies to RCCL or single handles, not in-process groups");
         h->rng_replicate = value != 0;

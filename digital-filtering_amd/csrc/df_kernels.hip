@@ -1049,9 +1049,11 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
     const int per_xcd = gridDim.x >> 3; // XCD-aware order, as ypass_kernel
     const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
     if (tile >= a.nstrips * Ny) return; // block-uniform
+    // rows in ascending order whatever heavy_first says: consecutive tiles of one XCD then share their
+    // noise rows in L2 (measured on the reference's grid: -8% against reversed rows, -18% against rows
+    // sorted by falling N; profiles/r2/ab_ycoop_native.jsonl)
     const int s = tile / Ny;
-    int j = tile - s * Ny;
-    if (a.heavy_first) j = Ny - 1 - j;
+    const int j = tile - s * Ny;
     const int N = a.Ny_st[c][(size_t)s * Ny + j];
     const int T = 2 * N + 1;
     const int col = s * kStrip + 2 * lane;
@@ -1120,8 +1122,18 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
     if (!table && a.ycoop) {
         const long long tiles = (long long)a.nstrips * a.Ny;
         const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);
-        if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 16>), grid, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((ypass_coop_kernel<false, 16>), grid, dim3(256), 0, st, a);
+        // ycoop 1: 16 taps per wave per chunk (64 KiB of LDS, 2 blocks per CU); 2: 8 taps (32 KiB, 4 blocks);
+        // 3: 4 taps (16 KiB, 8 blocks)
+        if (a.ycoop >= 3) {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 4>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop_kernel<false, 4>), grid, dim3(256), 0, st, a);
+        } else if (a.ycoop == 2) {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 8>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop_kernel<false, 8>), grid, dim3(256), 0, st, a);
+        } else {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 16>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop_kernel<false, 16>), grid, dim3(256), 0, st, a);
+        }
         return hipGetLastError();
     }
     switch (rows_per_wave) {

@@ -54,7 +54,8 @@ struct RngGeom {
     const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*(1024*(tid/64) + tid%64) outputs
     int Nz_g, Pz, z0, z1, is_first, is_last;
     uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
-    int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw
+    int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw,
+                                   // 8 no batches (compacted K3: the append loop alone)
     int nt_stores;                 // noise pairs stored non-temporally
     int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
                                    // iterations, so few-wave planes get short serial chains

@@ -509,51 +509,91 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
 // are skipped a batch at a time. Same draws, same arithmetic, same destinations: bit-identical.
 constexpr int kGenRing = 512; // slots per wave: < 64 carried + 4 iterations x 64 appended between flushes
 
-__device__ __forceinline__ void gen_batch(const RngGeom &g, const uint64_t *ring, int head, int n, long long rank0,
-                                          uint64_t f, long long A, RngStateDev *__restrict__ sout, int lane)
+// Wave-uniform lookups into the kernel argument's per-array tables as select chains over registers
+// loaded once, instead of one scalar load with a computed offset per use.
+template <class T, int K> __device__ __forceinline__ T sel(const T (&v)[K], int i)
 {
-    const long long rk = rank0 + head; // rank of the batch's first slot (uniform)
-    if (rk >= A) return;               // past the call's last attempt
-    const uint64_t qf = f + 2ull * (uint64_t)rk;
-    const StreamPos P0 = stream_pos(g, qf);
-    const int su = uniform(P0.sidx < 6 ? P0.sidx : 5);
-    const uint32_t left = (g.rows[su] - P0.row) * g.width[su] - P0.col;
-    const bool fast = P0.sidx < 6 && g.width[su] >= 2 * 64 && 2u * (uint32_t)n <= left;
-    const bool holds_last = rk <= A - 1 && A - 1 < rk + n;
-    if (fast && !holds_last) { // whole-batch skip: one row of one array, no column stored here
-        const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n, W = g.width[su];
-        if (c1 <= W) {
-            bool idle;
-            if (su & 1) {
-                const uint32_t nzp = (uint32_t)g.Nzp[su >> 1];
-                idle = (!g.is_first || c0 >= nzp) && (!g.is_last || c1 <= nzp + (uint32_t)g.Nz_g);
-            } else {
-                idle = c1 <= (uint32_t)g.z0 || c0 >= (uint32_t)g.z1;
-            }
-            if (idle) return;
+    T r = v[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) r = (i == k) ? v[k] : r;
+    return r;
+}
+
+// stream_advance with the select-chain tables (uniform, SALU).
+__device__ __forceinline__ StreamPos stream_advance_u(const RngGeom &g, StreamPos s, uint32_t d)
+{
+    while (d > 0 && s.sidx < 6) {
+        const uint32_t W = sel(g.width, s.sidx);
+        const uint32_t room = W - s.col;
+        if (d < room) {
+            s.col += d;
+            break;
         }
+        d -= room;
+        s.col = 0;
+        if (++s.row == sel(g.rows, s.sidx)) {
+            s.row = 0;
+            ++s.sidx;
+        }
+    }
+    return s;
+}
+
+// One batch: ring slots [head, head + n) hold the states of the wave's accepted attempts of ranks
+// rank0 + head ... (uniform), i.e. stream positions [qf, qf + 2n) starting at P (uniform).
+__device__ __forceinline__ void gen_batch(const RngGeom &g, const uint64_t *ring, int head, int n, long long rk,
+                                          const StreamPos P0, uint64_t f, long long A,
+                                          RngStateDev *__restrict__ sout, int lane)
+{
+    const uint64_t qf = f + 2ull * (uint64_t)rk;
+    const int su = P0.sidx < 6 ? P0.sidx : 5;
+    const uint32_t W = sel(g.width, su);
+    const uint32_t left = (sel(g.rows, su) - P0.row) * W - P0.col;
+    const bool fast = P0.sidx < 6 && W >= 2 * 64 && 2u * (uint32_t)n <= left;
+    const bool holds_last = rk <= A - 1 && A - 1 < rk + n;
+    // columns of array su this GPU stores: [lo1, hi1) at local column col + o1, [lo2, W) at col + o2
+    // (r_ys: this strip's columns; r_zs: the plane-edge pads, df.cpp:343-348, the interior never)
+    const int cmp = su >> 1;
+    const bool odd = su & 1;
+    const uint32_t nzp = (uint32_t)sel(g.Nzp, cmp);
+    const uint32_t lo1 = odd ? 0u : (uint32_t)g.z0;
+    const uint32_t hi1 = odd ? (g.is_first ? nzp : 0u) : (uint32_t)g.z1;
+    const uint32_t lo2 = odd && g.is_last ? nzp + (uint32_t)g.Nz_g : W;
+    const int o1 = odd ? 0 : -g.z0, o2 = -g.z0;
+    if (fast && !holds_last) { // whole-batch skip: one row of one array, no column stored here
+        const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n;
+        if (c1 <= W && (c1 <= lo1 || c0 >= hi1) && c1 <= lo2) return;
     }
     if (lane >= n) return;
     const long long rank = rk + lane;
     if (rank >= A) return;
     const uint64_t st = ring[(head + lane) & (kGenRing - 1)];
-    const uint64_t q0 = qf + 2ull * (uint64_t)lane;
     double *d0, *d1;
-    if (fast) { // one array, at most one row wrap: uniform array index, scalar tables
-        const uint32_t W = g.width[su];
-        StreamPos p0 = {su, P0.row, P0.col + 2u * (uint32_t)lane};
-        if (p0.col >= W) {
-            p0.col -= W;
-            p0.row++;
+    if (fast) { // one array, at most one row wrap
+        double *const base = odd ? sel(g.rz, cmp) : sel(g.ry, cmp);
+        const size_t pitch = odd ? (size_t)sel(g.rz_pitch, cmp) : (size_t)g.Pz;
+        double *const row0 = base + (size_t)P0.row * pitch;
+        uint32_t col = P0.col + 2u * (uint32_t)lane;
+        double *r = row0;
+        if (col >= W) {
+            col -= W;
+            r += pitch;
         }
-        StreamPos p1 = {su, p0.row, p0.col + 1u};
-        if (p1.col == W) {
-            p1.col = 0;
-            p1.row++;
+        uint32_t col1 = col + 1;
+        double *r1 = r;
+        if (col1 == W) {
+            col1 = 0;
+            r1 += pitch;
         }
-        d0 = stream_dest(g, p0);
-        d1 = stream_dest(g, p1);
+        auto dest = [&](double *rowp, uint32_t cc) -> double * {
+            if (cc >= lo1 && cc < hi1) return rowp + ((int)cc + o1);
+            if (cc >= lo2) return rowp + ((int)cc + o2);
+            return nullptr;
+        };
+        d0 = dest(r, col);
+        d1 = dest(r1, col1);
     } else {
+        const uint64_t q0 = qf + 2ull * (uint64_t)lane;
         const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
         d0 = stream_dest(g, p0);
         d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
@@ -618,6 +658,8 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     }
     const long long rank0 = rank_w; // rank of ring slot 0
     int tail = 0, head = 0;         // uniform
+    // stream position of slot `head` (uniform), advanced by 2n per batch
+    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)(rank0 < A ? rank0 : 0));
     for (int m = m0; m < m1; ++m) {
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
@@ -635,7 +677,11 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
             __asm__ volatile("" ::: "memory");
             while (tail - head >= 64 || (fin && tail > head)) {
                 const int n = min(64, tail - head);
-                if (!(g.debug_flags & 8)) gen_batch(g, ring, head, n, rank0, f, A, sout, lane);
+                const long long rk = rank0 + head;
+                if (rk < A && !(g.debug_flags & 8)) {
+                    gen_batch(g, ring, head, n, rk, P, f, A, sout, lane);
+                    P = stream_advance_u(g, P, 2u * (uint32_t)n);
+                }
                 head += n;
             }
             __asm__ volatile("" ::: "memory");

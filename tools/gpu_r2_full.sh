@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-2 full pass: GPU suite, smoke, the default bench line, rocprofv3 stats of the same command
+# (plus the per-grid split), and the c4 / c5 planes on one GPU with their parity checks.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+TAG=${1:-r2full}
+O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+  > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -60 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
+cat $O/smoke.log | tail -1
+timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err \
+  || { echo "bench failed"; tail -20 $O/bench_default.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('$O/bench_default.json'))
+print('c3', d['value'], d['ms_per_step'], 'parity', d['parity_ok'], 'frac', d['roofline']['frac'], d['roofline']['avg_launch_ms'])
+print('table', d['alt_modes']['table']['ms_per_step'], d['alt_modes']['table']['roofline_valu'])
+print({k:(v['ms_per_step'],v['parity_ok'],v['roofline']['frac']) for k,v in (d['other_configs'] or {}).items()})"
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof -o run -- \
+   python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 > $O/bench_under_rocprof.json 2> $O/prof.err) \
+   || { echo "rocprof failed"; tail -5 $O/prof.err; exit 1; }
+python3 tools/rocprof_split.py $O/prof/run_kernel_trace.csv > $O/kernel_split.csv
+head -12 $O/kernel_split.csv
+rm -f $O/prof/run_kernel_trace.csv
+for cfg in c4 c5; do
+  timeout -k 10 300 python bench.py --config $cfg --steps 10 --warmup 3 --cpu-baseline off --other-configs '' --alt-modes off \
+    > $O/bench_${cfg}_n1.json 2> $O/bench_${cfg}.err || { echo "bench $cfg failed"; tail -20 $O/bench_${cfg}.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/bench_${cfg}_n1.json')); print('$cfg', d['value'], d['ms_per_step'], d['parity_ok'], d['roofline']['frac'])"
+done

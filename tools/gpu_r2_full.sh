@@ -19,7 +19,7 @@ print('c3', d['value'], d['ms_per_step'], 'parity', d['parity_ok'], 'frac', d['r
 print('table', d['alt_modes']['table']['ms_per_step'], d['alt_modes']['table']['roofline_valu'])
 print({k:(v['ms_per_step'],v['parity_ok'],v['roofline']['frac']) for k,v in (d['other_configs'] or {}).items()})"
 export TMPDIR=/tmp
-(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof -o run -- \
+(cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
    python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 5 > $O/bench_under_rocprof.json 2> $O/prof.err) \
    || { echo "rocprof failed"; tail -5 $O/prof.err; exit 1; }
 python3 tools/rocprof_split.py $O/prof/run_kernel_trace.csv > $O/kernel_split.csv

@@ -519,87 +519,82 @@ template <class T, int K> __device__ __forceinline__ T sel(const T (&v)[K], int 
     return r;
 }
 
-// stream_advance with the select-chain tables (uniform, SALU).
-__device__ __forceinline__ StreamPos stream_advance_u(const RngGeom &g, StreamPos s, uint32_t d)
-{
-    while (d > 0 && s.sidx < 6) {
-        const uint32_t W = sel(g.width, s.sidx);
-        const uint32_t room = W - s.col;
-        if (d < room) {
-            s.col += d;
-            break;
-        }
-        d -= room;
-        s.col = 0;
-        if (++s.row == sel(g.rows, s.sidx)) {
-            s.row = 0;
-            ++s.sidx;
-        }
-    }
-    return s;
-}
+// Where a wave's accepted attempts store (uniform, computed once per wave): all of its stream
+// positions lie in array `su` starting at (row, col) unless `generic` (the run crosses an array end or
+// the rows are narrower than a batch: per-lane table lookups then). Columns this GPU stores: [lo1, hi1)
+// at local column col + o1 and [lo2, W) at col + o2 (r_ys: this strip's columns; r_zs: the plane-edge
+// pads, df.cpp:343-348; the r_zs interior, which df.cpp:377 overwrites, never).
+struct WaveDest {
+    double *base;
+    size_t pitch;
+    uint32_t W, row, col, lo1, hi1, lo2;
+    int o1, o2;
+    bool generic;
+};
 
-// One batch: ring slots [head, head + n) hold the states of the wave's accepted attempts of ranks
-// rank0 + head ... (uniform), i.e. stream positions [qf, qf + 2n) starting at P (uniform).
-__device__ __forceinline__ void gen_batch(const RngGeom &g, const uint64_t *ring, int head, int n, long long rk,
-                                          const StreamPos P0, uint64_t f, long long A,
-                                          RngStateDev *__restrict__ sout, int lane)
+__device__ __forceinline__ WaveDest wave_dest(const RngGeom &g, uint64_t q_lo, uint64_t n_pos)
 {
-    const uint64_t qf = f + 2ull * (uint64_t)rk;
-    const int su = P0.sidx < 6 ? P0.sidx : 5;
-    const uint32_t W = sel(g.width, su);
-    const uint32_t left = (sel(g.rows, su) - P0.row) * W - P0.col;
-    const bool fast = P0.sidx < 6 && W >= 2 * 64 && 2u * (uint32_t)n <= left;
-    const bool holds_last = rk <= A - 1 && A - 1 < rk + n;
-    // columns of array su this GPU stores: [lo1, hi1) at local column col + o1, [lo2, W) at col + o2
-    // (r_ys: this strip's columns; r_zs: the plane-edge pads, df.cpp:343-348, the interior never)
+    WaveDest w{};
+    const StreamPos P = stream_pos(g, q_lo);
+    const int su = P.sidx < 6 ? P.sidx : 5;
+    w.W = sel(g.width, su);
+    const uint64_t left = (uint64_t)(sel(g.rows, su) - P.row) * w.W - P.col;
+    w.generic = P.sidx >= 6 || w.W < 2 * 64 || n_pos > left;
     const int cmp = su >> 1;
     const bool odd = su & 1;
     const uint32_t nzp = (uint32_t)sel(g.Nzp, cmp);
-    const uint32_t lo1 = odd ? 0u : (uint32_t)g.z0;
-    const uint32_t hi1 = odd ? (g.is_first ? nzp : 0u) : (uint32_t)g.z1;
-    const uint32_t lo2 = odd && g.is_last ? nzp + (uint32_t)g.Nz_g : W;
-    const int o1 = odd ? 0 : -g.z0, o2 = -g.z0;
-    if (fast && !holds_last) { // whole-batch skip: one row of one array, no column stored here
-        const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n;
-        if (c1 <= W && (c1 <= lo1 || c0 >= hi1) && c1 <= lo2) return;
-    }
-    if (lane >= n) return;
+    w.base = odd ? sel(g.rz, cmp) : sel(g.ry, cmp);
+    w.pitch = odd ? (size_t)sel(g.rz_pitch, cmp) : (size_t)g.Pz;
+    w.row = P.row;
+    w.col = P.col;
+    w.lo1 = odd ? 0u : (uint32_t)g.z0;
+    w.hi1 = odd ? (g.is_first ? nzp : 0u) : (uint32_t)g.z1;
+    w.lo2 = odd && g.is_last ? nzp + (uint32_t)g.Nz_g : w.W;
+    w.o1 = odd ? 0 : -g.z0;
+    w.o2 = -g.z0;
+    return w;
+}
+
+// One batch: ring slots [head, head + n) hold the states of the wave's accepted attempts of ranks
+// rk + (0..n-1) (rk uniform), stream positions qw + 2 * (head + lane) from the wave's first one qw.
+__device__ __forceinline__ void gen_batch(const RngGeom &g, const WaveDest &w, const uint64_t *ring, int head, int n,
+                                          long long rk, uint64_t qw, uint64_t f, long long A,
+                                          RngStateDev *__restrict__ sout, int lane)
+{
     const long long rank = rk + lane;
-    if (rank >= A) return;
-    const uint64_t st = ring[(head + lane) & (kGenRing - 1)];
-    double *d0, *d1;
-    if (fast) { // one array, at most one row wrap
-        double *const base = odd ? sel(g.rz, cmp) : sel(g.ry, cmp);
-        const size_t pitch = odd ? (size_t)sel(g.rz_pitch, cmp) : (size_t)g.Pz;
-        double *const row0 = base + (size_t)P0.row * pitch;
-        uint32_t col = P0.col + 2u * (uint32_t)lane;
-        double *r = row0;
-        if (col >= W) {
-            col -= W;
-            r += pitch;
+    const bool live = lane < n && rank < A;
+    double *d0 = nullptr, *d1 = nullptr;
+    if (live) {
+        if (!w.generic) { // a few row wraps at most: the wave's run spans < 2048 positions, rows >= 128
+            uint32_t col = w.col + 2u * (uint32_t)(head + lane);
+            double *r = w.base + (size_t)w.row * w.pitch;
+            while (col >= w.W) {
+                col -= w.W;
+                r += w.pitch;
+            }
+            uint32_t col1 = col + 1;
+            double *r1 = r;
+            if (col1 == w.W) {
+                col1 = 0;
+                r1 += w.pitch;
+            }
+            auto dest = [&](double *rowp, uint32_t cc) -> double * {
+                if (cc >= w.lo1 && cc < w.hi1) return rowp + ((int)cc + w.o1);
+                if (cc >= w.lo2) return rowp + ((int)cc + w.o2);
+                return nullptr;
+            };
+            d0 = dest(r, col);
+            d1 = dest(r1, col1);
+        } else {
+            const uint64_t q0 = qw + 2ull * (uint64_t)(head + lane);
+            const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
+            d0 = stream_dest(g, p0);
+            d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
         }
-        uint32_t col1 = col + 1;
-        double *r1 = r;
-        if (col1 == W) {
-            col1 = 0;
-            r1 += pitch;
-        }
-        auto dest = [&](double *rowp, uint32_t cc) -> double * {
-            if (cc >= lo1 && cc < hi1) return rowp + ((int)cc + o1);
-            if (cc >= lo2) return rowp + ((int)cc + o2);
-            return nullptr;
-        };
-        d0 = dest(r, col);
-        d1 = dest(r1, col1);
-    } else {
-        const uint64_t q0 = qf + 2ull * (uint64_t)lane;
-        const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
-        d0 = stream_dest(g, p0);
-        d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
     }
-    const bool last = rank == A - 1;
-    if (!(d0 || d1 || last)) return;
+    const bool last = live && rank == A - 1;
+    if (!(d0 || d1 || last)) return; // the whole batch leaves at once where nothing is stored here
+    const uint64_t st = ring[(head + lane) & (kGenRing - 1)];
     uint64_t s4 = st;
     PolarAttempt a;
     if (g.debug_flags & 4) {
@@ -658,8 +653,12 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     }
     const long long rank0 = rank_w; // rank of ring slot 0
     int tail = 0, head = 0;         // uniform
-    // stream position of slot `head` (uniform), advanced by 2n per batch
-    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)(rank0 < A ? rank0 : 0));
+    // this wave's positions: [qw, qw + 2 * (accepted attempts in iterations m0..m1-1)), within the call
+    const uint64_t qw = f + 2ull * (uint64_t)(rank0 < A ? rank0 : 0);
+    uint32_t nacc = 0;
+    for (int m = m0; m < m1; ++m) nacc += (uint32_t)__popcll(__ballot((bits >> m) & 1u));
+    const uint64_t q_end = min(qw + 2ull * nacc, (uint64_t)g.Q);
+    const WaveDest wd = wave_dest(g, qw, q_end > qw ? q_end - qw : 0);
     for (int m = m0; m < m1; ++m) {
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
@@ -678,10 +677,7 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
             while (tail - head >= 64 || (fin && tail > head)) {
                 const int n = min(64, tail - head);
                 const long long rk = rank0 + head;
-                if (rk < A && !(g.debug_flags & 8)) {
-                    gen_batch(g, ring, head, n, rk, P, f, A, sout, lane);
-                    P = stream_advance_u(g, P, 2u * (uint32_t)n);
-                }
+                if (rk < A && !(g.debug_flags & 8)) gen_batch(g, wd, ring, head, n, rk, qw, f, A, sout, lane);
                 head += n;
             }
             __asm__ volatile("" ::: "memory");

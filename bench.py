@@ -233,12 +233,24 @@ def make_filter(dfamd, ctx, wl, args, coeff_mode, split=True, comm_id=None):
     return dfamd.DigitalFilter(**kw)
 
 
-def timed(ctx, h, args):
-    """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile."""
+def timed(ctx, h, args, min_warm_s=0.0):
+    """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile.
+    min_warm_s > 0 (secondary lines only: alt mode, other configs) keeps warming up until that much
+    time has passed: a 0.4 ms table-mode call otherwise starts timing while the clocks still ramp
+    (c3 table: 0.395 ms/call after 5 calls, 0.370 after 140; profiles/r2/table_warmup.txt)."""
     torch = ctx.torch
+    calls = 0
     for _ in range(args.warmup):
         h.filter(args.dt)
+        calls += 1
     h.sync()
+    t_w = time.perf_counter()
+    # one process only: every call of a split plane is an RCCL exchange, so ranks must run equal counts
+    while min_warm_s > 0 and ctx.world == 1 and time.perf_counter() - t_w < min_warm_s:
+        for _ in range(10):
+            h.filter(args.dt)
+            calls += 1
+        h.sync()
     h.set_profiling(True)
     ctx.barrier()
     torch.cuda.synchronize()
@@ -251,7 +263,7 @@ def timed(ctx, h, args):
     el = time.perf_counter() - t0
     prof = h.profile()
     h.set_profiling(False)
-    return el, prof
+    return el, prof, calls + args.steps
 
 
 def per_call(prof):
@@ -319,12 +331,13 @@ def roofline_of(h, prof, args, config_name):
     return r
 
 
-def run_config(dfamd, ctx, wl, args, comm_id):
-    """Create, time and parity-check one workload on every rank. Returns the rank-0 view."""
+def run_config(dfamd, ctx, wl, args, comm_id, min_warm_s=0.0):
+    """Create and time one workload on every rank; returns the handle and this rank's record."""
     t_setup = time.perf_counter()
     f = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
     t_setup = time.perf_counter() - t_setup
-    elapsed, prof = timed(ctx, f, args)
+    elapsed, prof, ncalls = timed(ctx, f, args, min_warm_s)
+    f.calls_done = ncalls  # filter(dt) calls after step 0, for the parity reference
     rank_rec = {"rank": ctx.rank, "elapsed_s": elapsed, "phase_ms_per_call": per_call(prof),
                 "roofline": roofline_of(f, prof, args, wl["name"]), "columns": [f.z0, f.z1],
                 "comm": f.comm_info() if ctx.world > 1 else None, "setup_s": round(t_setup, 3),
@@ -384,21 +397,18 @@ def main(argv=None):
     f, rec = run_config(dfamd, ctx, wl, args, comm_id)
     recs = ctx.gather(rec)
     head = summarize(ctx, wl, args, recs)
-    calls_done = args.warmup + args.steps  # filter(dt) calls after the constructor's step 0
 
     alt = None
-    ref_for_parity = None
     if ctx.world == 1 and args.alt_modes == "auto" and wl["plane"] != "native":
         other = "table" if args.coeff_mode == "packed" else "packed"
         g = make_filter(dfamd, ctx, wl, args, other)
         taps = sum(g.comp_info(c)["by_size"] + g.comp_info(c)["bz_size"] for c in range(3))
-        el2, p2 = timed(ctx, g, args)
+        el2, p2, _ = timed(ctx, g, args, min_warm_s=0.3)
         ms2 = el2 * 1e3 / args.steps
         cells = wl["Ny"] * wl["Nz"]
         alt = {other: {"value": round(cells * args.steps / el2, 1), "ms_per_step": round(ms2, 4),
                        "phase_ms_per_call": per_call(p2)}}
         if other == "table":
-            ref_for_parity = g  # same seed, same calls: the unsplit table-mode reference of the parity check
             alt[other]["note"] = ("same results bit for bit (parity below, tests/test_gpu_parity.py); coefficients "
                                   "read from a per-N table instead of the offset-packed stream, so SURVEY 8d's "
                                   "algorithmic bytes do not apply: FP64-VALU roofline below")
@@ -417,17 +427,14 @@ def main(argv=None):
                 ceil_tf = best * 64 / 1e12
                 alt[other]["roofline_valu"]["measured_ceiling"] = {
                     "TFLOPs": round(ceil_tf, 1), "frac": round(tf / ceil_tf, 4), "source": os.path.relpath(vp, ROOT)}
-        else:
-            g.close()
+        g.close()
 
     parity = None
     if args.parity == "on":
-        pr = parity_check(dfamd, ctx, wl, args, f, calls_done, ref=ref_for_parity)
+        pr = parity_check(dfamd, ctx, wl, args, f, f.calls_done)
         prs = ctx.gather(pr)
         parity = {"ok": all(p["ok"] for p in prs), "reference": "whole plane, one GPU, table mode, same seed/calls",
-                  "calls_compared": calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
-    if ref_for_parity is not None:
-        ref_for_parity.close()
+                  "calls_compared": f.calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
     comm = f.comm_info() if ctx.world > 1 else None
     f.close()
 
@@ -439,12 +446,12 @@ def main(argv=None):
             owl = plan_workload(oname, ctx.world, args.scaling)
         except ValueError:
             continue
-        h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd))
+        h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd), min_warm_s=0.3)
         orecs = ctx.gather(orec)
         osum = summarize(ctx, owl, args, orecs)
         op = ops = None
         if args.parity == "on":
-            ops = ctx.gather(parity_check(dfamd, ctx, owl, args, h, calls_done))
+            ops = ctx.gather(parity_check(dfamd, ctx, owl, args, h, h.calls_done))
             op = all(p["ok"] for p in ops)
         h.close()
         others[oname] = {"workload": owl["desc"], "Ny": owl["Ny"], "Nz": owl["Nz"], "scaling": owl["scaling"],

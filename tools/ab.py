@@ -21,6 +21,10 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
+if "--torch" in sys.argv:  # bind libdfamd to torch's HIP runtime first, as bench.py does
+    sys.argv.remove("--torch")
+    import torch  # noqa: F401
+    torch.cuda.set_device(0)
 import dfamd  # noqa: E402
 
 CFG = {"c1": (128, 128, 8, 8), "c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64), "c5": (4096, 4096, 4, 64),

@@ -1234,8 +1234,6 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         }
     }
     if (col >= a.Nz_loc) return; // padding lanes (after their share of the staging copy)
-    int vzero = 0; // 0 in a VGPR: addresses built on it are per-lane to the compiler (vector loads)
-    if (TABLE) __asm__ volatile("v_mov_b32 %0, 0" : "=v"(vzero));
 
     double f0[3], f1[3];
 #pragma unroll
@@ -1325,70 +1323,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         r0 = acc0;
         r1 = acc1;
         };
-        if (TABLE && !PC && staged && a.zpipe && N >= 4) {
-            // Software-pipelined taps (SweepArgs::zpipe): the next 8 taps' noise pairs (LDS) and coefficient
-            // pairs are issued before the current 8 taps' arithmetic. The coefficients come through the
-            // vector memory path (a per-lane-looking address): scalar loads share lgkmcnt with the LDS reads
-            // and return out of order, which forces a full lgkmcnt(0) wait on every iteration. Same
-            // products and sums in the same order as `taps`: bit-identical.
-            const lds_pair_ptr xp = (lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane);
-            const dvec2 *cp = reinterpret_cast<const dvec2 *>(tb + vzero); // pair k = taps 2k, 2k+1
-            double acc0 = 0.0, acc1 = 0.0;
-            double2 P = ld_pair(xp), Q[4];
-            dvec2 cq[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                Q[u] = ld_pair(xp + 1 + u);
-                cq[u] = cp[u];
-            }
-            auto body8 = [&](const double2 P0, const double2 *Qv, const dvec2 *cv) {
-                acc0 += cv[0].x * P0.x;
-                acc1 += cv[0].x * P0.y;
-                acc0 += cv[0].y * P0.y;
-                acc1 += cv[0].y * Qv[0].x;
-#pragma unroll
-                for (int u = 1; u < 4; ++u) {
-                    acc0 += cv[u].x * Qv[u - 1].x;
-                    acc1 += cv[u].x * Qv[u - 1].y;
-                    acc0 += cv[u].y * Qv[u - 1].y;
-                    acc1 += cv[u].y * Qv[u].x;
-                }
-            };
-            int m = 0;
-            for (; m + 8 <= N; m += 4) {
-                double2 R[4];
-                dvec2 cr[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    R[u] = ld_pair(xp + m + 5 + u);
-                    cr[u] = cp[(m + 4) + u];
-                }
-                body8(P, Q, cq);
-                P = Q[3];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    Q[u] = R[u];
-                    cq[u] = cr[u];
-                }
-            }
-            body8(P, Q, cq); // the window prefetched last: pairs up to m + 4 <= N
-            P = Q[3];
-            m += 4;
-            for (; m < N; ++m) {
-                const double2 P1 = ld_pair(xp + m + 1);
-                const double b0 = DF_TCOEF(tb[2 * m]), b1 = DF_TCOEF(tb[2 * m + 1]);
-                acc0 += b0 * P.x;
-                acc1 += b0 * P.y;
-                acc0 += b1 * P.y;
-                acc1 += b1 * P1.x;
-                P = P1;
-            }
-            const double bl = DF_TCOEF(tb[2 * N]);
-            acc0 += bl * P.x;
-            acc1 += bl * P.y;
-            f0[c] = acc0;
-            f1[c] = acc1;
-        } else if (TABLE && !PC && staged) {
+        if (TABLE && !PC && staged) {
             taps((lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane), f0[c], f1[c]);
         } else {
             taps(gxp, f0[c], f1[c]);

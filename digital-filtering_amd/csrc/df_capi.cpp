@@ -703,6 +703,8 @@ int plan_rng(df_handle *h)
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
     g.gen_compact = 1;
+    g.fast_log = 1; // table-driven log in the polar transform (within 1 ulp of glibc; tests/test_rng_log.py)
+    if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
     g.nt_stores = 1; // noise written past the caches: it is read once, by the next call's sweeps (A/B -1.4%)
     const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
@@ -931,6 +933,14 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         if ((rc = upload(h, djt, jt.data(), jt.size()))) return rc;
         h->geom.jump_block = djb;
         h->geom.jump_thread = djt;
+    }
+    {
+        std::vector<LogTabEntry> lt(kLogTab);
+        build_log_table(lt.data());
+        LogTabEntry *dlt = nullptr;
+        if ((rc = dalloc_t(h, &dlt, lt.size()))) return rc;
+        if ((rc = upload(h, dlt, lt.data(), lt.size()))) return rc;
+        h->geom.log_tab = dlt;
     }
     HIP_OR(hipHostMalloc((void **)&h->err_host, 3 * sizeof(int), hipHostMallocMapped), DF_EHIP);
     h->err_host[0] = h->err_host[1] = h->err_host[2] = 0;
@@ -1566,6 +1576,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
+    else if (k == "fast_log") h->geom.fast_log = value != 0;
     else if (k == "graph") h->use_graph = value != 0;
     else if (k == "ywin_T" || k == "zwin_T") {
         if (value < 0 || value > (1 << 24) || (value & (value - 1)))

@@ -472,7 +472,7 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
                     } else {
                         a = polar_attempt(s4); // same draws K1 tested
                     }
-                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * log(a.r2) / a.r2);
+                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * (g.fast_log ? log_r2(a.r2, g.log_tab) : log(a.r2)) / a.r2);
                     const double xm = a.x * mult;
                     const double ym = a.y * mult;
                     const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;
@@ -605,7 +605,7 @@ __device__ __forceinline__ void gen_batch(const RngGeom &g, const WaveDest &w, c
     } else {
         a = polar_attempt(s4); // the draws K1 tested
     }
-    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * log(a.r2) / a.r2);
+    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * (g.fast_log ? log_r2(a.r2, g.log_tab) : log(a.r2)) / a.r2);
     const double xm = a.x * mult;
     const double ym = a.y * mult;
     const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;

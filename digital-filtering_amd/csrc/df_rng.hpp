@@ -11,6 +11,7 @@
 // Every floating-point line is written so that no FMA can be formed (the library
 // is compiled with -ffp-contract=off), matching the reference's x86-64 -O2 code.
 #pragma once
+#include <cmath>
 #include <cstdint>
 
 #ifdef __HIPCC__
@@ -117,6 +118,68 @@ DF_HD int polar_screen(uint64_t s0)
     if (r2f > 1e-5f && r2f < 1.0f - 1e-5f) return 1;
     if (r2f > 1.0f + 1e-5f) return 0;
     return -1;
+}
+
+// ---- log(r2) for the polar transform, r2 in (0, 1] (a normal double: r2 >= 2^-106 > DBL_MIN).
+// Table-driven (Tang): r2 = 2^k * m with m in [sqrt(1/2), sqrt(2)); c = the centre of m's cell (width
+// 1/256 below 1, 1/128 above; c = 1 exactly for the two cells around 1, so log(1) = 0 and r2 -> 1 has
+// no cancellation); r = m * (1/c) - 1 by one FMA, |r| < 2^-7; log(m) = -log(1/c) + log1p(r), log1p by a
+// degree-8 polynomial (truncation < 2^-59 relative). k*ln2_hi + T_hi is exact (both on a 2^-43 grid),
+// the rest is added small to large. ~25 VALU against ~85 for the device library's log; error about
+// 0.5 ulp, within 1 ulp of glibc's log (tests/test_rng_log.py: 2e7 arguments, and the GPU normals
+// stay within 2 ulp of the reference's). The host builds the table (build_log_table).
+struct LogTabEntry {
+    double rinv, thi, tlo, pad; // 1/c rounded; -log(rinv) = thi + tlo, thi on the 2^-43 grid
+};
+constexpr int kLogTab = 256;     // index: top 7 mantissa bits, +128 in the [1, sqrt 2) binade
+constexpr double kLn2Hi = 0x1.62e42fefa3800p-1; // ln 2 on the 2^-43 grid
+constexpr double kLn2Lo = 0x1.ef35793c76730p-45; // ln 2 - kLn2Hi
+
+DF_HD uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
+DF_HD double dfrom(uint64_t b) { return __builtin_bit_cast(double, b); }
+
+DF_HD double log_r2(double x, const LogTabEntry *tab)
+{
+    uint64_t mb = (dbits(x) & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull; // m in [1, 2)
+    int k = (int)(dbits(x) >> 52) - 1023;
+    const bool fold = mb >= 0x3FF6A09E667F3BCDull; // m >= sqrt(2): m / 2, k + 1 (exponent field only)
+    if (fold) {
+        mb -= 0x0010000000000000ull;
+        k += 1;
+    }
+    const LogTabEntry &e = tab[(int)((mb >> 45) & 0x7F) + (fold ? 0 : 128)];
+    const double m = dfrom(mb);
+    const double r = fma(m, e.rinv, -1.0);
+    const double r2 = r * r;
+    double q = fma(r, -0.125, 0x1.2492492492492p-3);  // 1/7
+    q = fma(r, q, -0x1.5555555555555p-3);             // -1/6
+    q = fma(r, q, 0x1.999999999999ap-3);              // 1/5
+    q = fma(r, q, -0.25);
+    q = fma(r, q, 0x1.5555555555555p-2);              // 1/3
+    q = fma(r, q, -0.5);
+    const double p = r2 * q;
+    const double dk = (double)k;
+    const double hi = fma(dk, kLn2Hi, e.thi);          // exact
+    const double lo = fma(dk, kLn2Lo, e.tlo);
+    return hi + (r + (p + lo));
+}
+
+// The log_r2 table (host): cell centres, 1/c rounded to double, -log(1/c) in x87 long double
+// (64-bit significand) split into a 2^-43-grid head and a tail.
+inline void build_log_table(LogTabEntry *tab)
+{
+    for (int idx = 0; idx < kLogTab; ++idx) {
+        const bool fold = idx < 128;
+        const int j = idx & 127;
+        double c;
+        if (fold) c = (j == 127) ? 1.0 : 0.5 * (1.0 + (j + 0.5) / 128.0);
+        else c = (j == 0) ? 1.0 : 1.0 + (j + 0.5) / 128.0;
+        const double rinv = 1.0 / c;
+        const long double T = -logl((long double)rinv);
+        const long double grid = 8796093022208.0L; // 2^43
+        const double thi = (double)(nearbyintl(T * grid) / grid);
+        tab[idx] = LogTabEntry{rinv, thi, (double)(T - (long double)thi), 0.0};
+    }
 }
 
 } // namespace dfamd

@@ -64,7 +64,10 @@ def test_rng_stream_state_bitexact(spec):
         assert g.rng_state() == o.rng.state
 
 
-def test_noise_arrays_match_oracle():
+@pytest.mark.parametrize("fast_log", ["1", "0"])
+def test_noise_arrays_match_oracle(monkeypatch, fast_log):
+    # fast_log 1 (default): K3's table-driven log (df_rng.hpp log_r2); 0: the device library's log
+    monkeypatch.setenv("DFAMD_FAST_LOG", fast_log)
     spec = (64, 200, 2, 12)
     o = oracle_synth(*spec, seed=11)
     g = gpu_synth(*spec, seed=11)
@@ -218,7 +221,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(rows_per_wave=2, yunroll=8, nt_loads=1), dict(gen_split=1), dict(gen_split=4),
                 dict(gen_split=16), dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256),
                 dict(ywin_T=0, zwin_T=4096, zwin_W=0), dict(ycoop=1), dict(gen_compact=0, ycoop=0),
-                dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0)]
+                dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0),
+                dict(fast_log=0), dict(fast_log=1)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

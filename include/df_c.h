@@ -189,7 +189,9 @@ int df_plane_info(df_handle *h, int *plane, int *per_cell);
 int df_gather_field(df_handle *h, int which, long long n, const long long *plane_cell, double *dst,
                     const long long *dst_cell, long long dst_len, double beta);
 
-/* Launch-shape tuning (extension; results are bit-identical for every setting):
+/* Launch-shape tuning (extension; results are bit-identical for every setting except "fast_log":
+ * 1 (default) = the table-driven log of the polar transform, 0 = the device math library's log; the
+ * two differ by at most 1 ulp in log(r2), both within 2 ulp of the reference's normals):
  * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4; 8 = 8-deep load pipeline),
  * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS),
  * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "graph" (steady-state

@@ -221,8 +221,7 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(rows_per_wave=2, yunroll=8, nt_loads=1), dict(gen_split=1), dict(gen_split=4),
                 dict(gen_split=16), dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256),
                 dict(ywin_T=0, zwin_T=4096, zwin_W=0), dict(ycoop=1), dict(gen_compact=0, ycoop=0),
-                dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0),
-                dict(fast_log=0), dict(fast_log=1)]
+                dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

@@ -710,6 +710,11 @@ int plan_rng(df_handle *h)
     const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
     g.next_mult = next.mult;
     g.next_plus = next.plus;
+    { // s_k = A_k s0 + C_k (k steps): the next attempt's s_k = J s_k + (A_k C_J + C_k - J C_k)
+        const PcgJump j1 = pcg_jump(1), j3 = pcg_jump(3);
+        g.next_plus1 = j1.mult * next.plus + j1.plus - next.mult * j1.plus;
+        g.next_plus3 = j3.mult * next.plus + j3.plus - next.mult * j3.plus;
+    }
     g.Nz_g = s.Nz;
     g.Pz = h->Pz;
     g.z0 = h->z0;

@@ -126,15 +126,20 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
         if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
         return;
     }
-    uint64_t st = thread_first_state(g, sin->state, gb, tid);
-    const uint64_t st0 = st;
+    const uint64_t st0 = thread_first_state(g, sin->state, gb, tid);
+    // The screen reads outputs 1 and 3 of each attempt only: the lane walks the states one and three
+    // steps into its attempts directly, each with one 64-bit multiply-add per attempt (J s + P_k, the
+    // 256-step jump conjugated: J and the step commute), instead of the attempt start plus two steps.
+    uint64_t s1 = st0 * kPcgMult + kPcgInc;
+    uint64_t s3 = s1 * kPcgMult2 + kPcgInc2;
     uint32_t bits = 0, unsure = 0;
 #pragma unroll 4
     for (int m = 0; m < kRngPerThread; ++m) {
-        const int v = polar_screen(st); // st stays at the attempt's start
+        const int v = polar_screen13(s1, s3);
         bits |= (v > 0 ? 1u : 0u) << m;
         unsure |= (v < 0 ? 1u : 0u) << m;
-        st = g.next_mult * st + g.next_plus; // the lane's next attempt, 64 attempts on
+        s1 = g.next_mult * s1 + g.next_plus1; // the lane's next attempt, 64 attempts on
+        s3 = g.next_mult * s3 + g.next_plus3;
     }
     // ~2e-5 of the attempts: the exact double test of polar_attempt (random.tcc:1822-1826)
     while (unsure) {

@@ -52,6 +52,7 @@ struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
     uint64_t next_mult, next_plus; // jump over 64*4 outputs (attempt start to the lane's next one)
+    uint64_t next_plus1, next_plus3; // the same jump for the states 1 and 3 steps into an attempt (K1)
     const PcgJumpDev *jump_block;  // [nblocks]: jump over 4*4096*b outputs
     const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*(1024*(tid/64) + tid%64) outputs
     int Nz_g, Pz, z0, z1, is_first, is_last;

@@ -108,16 +108,21 @@ constexpr uint64_t kPcgInc2 = 0x1a08ee1184ba6d32ULL;
 // only the high words o[1] = output(s1) and o[3] = output(s3), i.e. two 64-bit multiply-adds (s1 = one
 // step, s3 = two more) and two outputs instead of four of each. Returns 1 (accept), 0 (reject) or -1
 // (within 1e-5 of the circle or the origin: the caller redoes the exact double test, polar_attempt).
-DF_HD int polar_screen(uint64_t s0)
+// The same screen from the states s1, s3 (1 and 3 steps after the attempt's start) directly.
+DF_HD int polar_screen13(uint64_t s1, uint64_t s3)
 {
-    const uint64_t s1 = s0 * kPcgMult + kPcgInc;
-    const uint64_t s3 = s1 * kPcgMult2 + kPcgInc2;
     const float xf = (float)pcg_output(s1) * 4.656612873077392578125e-10f - 1.0f; // 2^-31
     const float yf = (float)pcg_output(s3) * 4.656612873077392578125e-10f - 1.0f;
     const float r2f = xf * xf + yf * yf;
     if (r2f > 1e-5f && r2f < 1.0f - 1e-5f) return 1;
     if (r2f > 1.0f + 1e-5f) return 0;
     return -1;
+}
+
+DF_HD int polar_screen(uint64_t s0)
+{
+    const uint64_t s1 = s0 * kPcgMult + kPcgInc;
+    return polar_screen13(s1, s1 * kPcgMult2 + kPcgInc2);
 }
 
 // ---- log(r2) for the polar transform, r2 in (0, 1] (a normal double: r2 >= 2^-106 > DBL_MIN).

@@ -1197,7 +1197,7 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 // x[col+1+i]. With N even, pairs P_m = (x[col-N+2m], x[col-N+2m+1]) are 16-B
 // aligned: even tap -N+2m uses P_m, odd tap -N+2m+1 uses (P_m.y, P_{m+1}.x), so
 // one 16-B noise load serves two taps and the order i = -N..N is unchanged.
-template <bool TABLE, bool NT, int ZU, bool PC, bool ZP = false>
+template <bool TABLE, bool NT, int ZU, bool PC>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
@@ -1239,8 +1239,6 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         }
     }
     if (col >= a.Nz_loc) return; // padding lanes (after their share of the staging copy)
-    int vzero = 0; // ZP: 0 in a VGPR, so addresses built on it are per-lane to the compiler (vector loads)
-    if (ZP) __asm__ volatile("v_mov_b32 %0, 0" : "=v"(vzero));
 
     double f0[3], f1[3];
 #pragma unroll
@@ -1330,70 +1328,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         r0 = acc0;
         r1 = acc1;
         };
-        if (ZP && TABLE && !PC && staged && N >= 4) {
-            // Software-pipelined taps (SweepArgs::zpipe, its own instantiation): the next 8 taps' noise pairs
-            // (LDS) and coefficient pairs are issued before the current 8 taps' arithmetic. The coefficients
-            // come through the vector memory path: scalar loads share lgkmcnt with the LDS reads and return
-            // out of order, which forces a full lgkmcnt(0) wait in every iteration. Same products and sums
-            // in the same order as `taps`: bit-identical.
-            const lds_pair_ptr xp = (lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane);
-            const dvec2 *cp = reinterpret_cast<const dvec2 *>(tb + vzero); // pair k = taps 2k, 2k+1
-            double acc0 = 0.0, acc1 = 0.0;
-            double2 P = ld_pair(xp), Q[4];
-            dvec2 cq[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                Q[u] = ld_pair(xp + 1 + u);
-                cq[u] = cp[u];
-            }
-            auto body8 = [&](const double2 P0, const double2 *Qv, const dvec2 *cv) {
-                acc0 += cv[0].x * P0.x;
-                acc1 += cv[0].x * P0.y;
-                acc0 += cv[0].y * P0.y;
-                acc1 += cv[0].y * Qv[0].x;
-#pragma unroll
-                for (int u = 1; u < 4; ++u) {
-                    acc0 += cv[u].x * Qv[u - 1].x;
-                    acc1 += cv[u].x * Qv[u - 1].y;
-                    acc0 += cv[u].y * Qv[u - 1].y;
-                    acc1 += cv[u].y * Qv[u].x;
-                }
-            };
-            int m = 0;
-            for (; m + 8 <= N; m += 4) {
-                double2 R[4];
-                dvec2 cr[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    R[u] = ld_pair(xp + m + 5 + u);
-                    cr[u] = cp[(m + 4) + u];
-                }
-                body8(P, Q, cq);
-                P = Q[3];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    Q[u] = R[u];
-                    cq[u] = cr[u];
-                }
-            }
-            body8(P, Q, cq); // the window prefetched last: pairs up to m + 4 <= N
-            P = Q[3];
-            m += 4;
-            for (; m < N; ++m) {
-                const double2 P1 = ld_pair(xp + m + 1);
-                const double b0 = DF_TCOEF(tb[2 * m]), b1 = DF_TCOEF(tb[2 * m + 1]);
-                acc0 += b0 * P.x;
-                acc1 += b0 * P.y;
-                acc0 += b1 * P.y;
-                acc1 += b1 * P1.x;
-                P = P1;
-            }
-            const double bl = DF_TCOEF(tb[2 * N]);
-            acc0 += bl * P.x;
-            acc1 += bl * P.y;
-            f0[c] = acc0;
-            f1[c] = acc1;
-        } else if (TABLE && !PC && staged) {
+        if (TABLE && !PC && staged) {
             taps((lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane), f0[c], f1[c]);
         } else {
             taps(gxp, f0[c], f1[c]);
@@ -1487,8 +1422,7 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
         const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
-        if (a.zpipe && a.zstage) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false, true>), dim3(blocks), dim3(256), lds, st, a);
-        else if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
     } else if (a.nt_loads) {
         if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);

@@ -331,24 +331,14 @@ def roofline_of(h, prof, args, config_name):
     return r
 
 
-def run_config(dfamd, ctx, wl, args, comm_id, min_warm_s=0.0, secondary=False):
-    """Create and time one workload on every rank; returns the handle and this rank's record.
-    secondary (other configs, one process): the wall time comes from a pass without per-phase events
-    (small planes are bound by the host's launch rate, which 6 event records per call lower) and the
-    phases and roofline from a second, profiled pass of K calls."""
+def run_config(dfamd, ctx, wl, args, comm_id, min_warm_s=0.0):
+    """Create and time one workload on every rank; returns the handle and this rank's record."""
     t_setup = time.perf_counter()
     f = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
     t_setup = time.perf_counter() - t_setup
-    if secondary and ctx.world == 1:
-        elapsed, _, n0 = timed(ctx, f, args, min_warm_s, profile=False)
-        el_prof, prof, n1 = timed(ctx, f, args)
-        ncalls = n0 + n1
-    else:
-        elapsed, prof, ncalls = timed(ctx, f, args, min_warm_s)
-        el_prof = elapsed
+    elapsed, prof, ncalls = timed(ctx, f, args, min_warm_s)
     f.calls_done = ncalls  # filter(dt) calls after step 0, for the parity reference
-    rank_rec = {"rank": ctx.rank, "elapsed_s": elapsed, "elapsed_profiled_s": el_prof,
-                "phase_ms_per_call": per_call(prof),
+    rank_rec = {"rank": ctx.rank, "elapsed_s": elapsed, "phase_ms_per_call": per_call(prof),
                 "roofline": roofline_of(f, prof, args, wl["name"]), "columns": [f.z0, f.z1],
                 "comm": f.comm_info() if ctx.world > 1 else None, "setup_s": round(t_setup, 3),
                 "call_bytes": f.algorithmic_bytes(-1)}
@@ -460,7 +450,7 @@ def main(argv=None):
             owl = plan_workload(oname, ctx.world, args.scaling)
         except ValueError:
             continue
-        h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd), min_warm_s=0.3, secondary=True)
+        h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd), min_warm_s=0.3)
         orecs = ctx.gather(orec)
         osum = summarize(ctx, owl, args, orecs)
         op = ops = None
@@ -469,9 +459,7 @@ def main(argv=None):
             op = all(p["ok"] for p in ops)
         h.close()
         others[oname] = {"workload": owl["desc"], "Ny": owl["Ny"], "Nz": owl["Nz"], "scaling": owl["scaling"],
-                         "parity_ok": op, **osum,
-                         "ms_per_step_with_phase_events": round(max(r["elapsed_profiled_s"] for r in orecs)
-                                                                * 1e3 / args.steps, 4)}
+                         "parity_ok": op, **osum}
         if ops and not op:
             others[oname]["parity"] = [p for p in ops if not p["ok"]]
         if oname == "c5":

@@ -1084,7 +1084,7 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 // Every product and every addition is the one the per-wave kernel performs, in the same order
 // i = -N..N: bit-identical. On the reference's own grid (N_y up to 212, ~6 tiles per SIMD) a wave's
 // serial chain of 2N+1 dependent load rounds, not HBM bandwidth, set the per-wave kernel's time.
-template <bool NT, int KPW, bool TABLE = false>
+template <bool NT, int KPW>
 __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
 {
     constexpr int CH = 4 * KPW; // taps per chunk
@@ -1105,10 +1105,7 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
     const int T = 2 * N + 1;
     const int col = s * kStrip + 2 * lane;
     const bool live = col < a.Nz_loc;
-    // packed: tap t of the lane's two cells at bp + t*128; table (row-uniform N): the tile's one
-    // coefficient of tap t at tb[t] (full symmetric vector, a scalar load)
-    const double *bp = TABLE ? nullptr : a.By[c] + a.byoff[c][(size_t)s * Ny + j] + 2 * lane;
-    const double *tb = TABLE ? a.tabf + a.tabf_off[N] : nullptr;
+    const double *bp = a.By[c] + a.byoff[c][(size_t)s * Ny + j] + 2 * lane;       // tap t at bp + t*128
     const double *np = a.ry[c] + (size_t)(j + a.Nyp[c] - N) * a.Pz + col;          // tap t at np + t*Pz
     double acc = 0.0; // thread k < 128: cell s*128 + k
     for (int t0 = 0; t0 < T; t0 += CH) {
@@ -1117,12 +1114,7 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
         for (int k = 0; k < KPW; ++k) {
             const int t = t0 + w + 4 * k;
             if (live && t < T) {
-                if (TABLE) {
-                    const double bv = DF_TCOEF(tb[t]);
-                    b[k] = make_double2(bv, bv);
-                } else {
-                    b[k] = ldB<NT>(bp + (ptrdiff_t)t * kStrip);
-                }
+                b[k] = ldB<NT>(bp + (ptrdiff_t)t * kStrip);
                 n[k] = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * a.Pz), t);
             } else {
                 b[k] = n[k] = make_double2(0.0, 0.0);
@@ -1174,12 +1166,6 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
-    if (a.ycoop && table && !a.per_cell) { // table mode, row-uniform N: 8 taps per wave per chunk
-        const long long tiles = (long long)a.nstrips * a.Ny;
-        const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);
-        hipLaunchKernelGGL((ypass_coop_kernel<false, 8, true>), grid, dim3(256), 0, st, a);
-        return hipGetLastError();
-    }
     if (!table && a.ycoop) {
         const long long tiles = (long long)a.nstrips * a.Ny;
         const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);

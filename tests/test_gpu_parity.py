@@ -136,7 +136,6 @@ def test_golden_synthetic(name):
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8, ycoop=0)),
                                          ("packed", dict(ycoop=1)), ("packed", dict(ycoop=3)), ("table", dict(yunroll=8)),
-                                         ("table", dict(ycoop=2)), ("table", dict(ycoop=0)),
                                          ("table", dict(gen_compact=0))])
 def test_golden_native_grid(mode, tuning):
     # the reference's own grid (N_y up to 212): default shapes and the deep y-pass pipeline

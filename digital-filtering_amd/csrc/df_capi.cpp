@@ -100,6 +100,7 @@ struct df_handle {
     int zstage = 1;    // table z-pass noise staged in LDS
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
+    int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     // z-strips: every rank counts every attempt block, so the halo send/recv is the call's only
     // collective (SURVEY 8e option B, north star "single RCCL halo exchange"). 0 = split counting
     // plus a per-call all-gather of counts and accept masks (option A), ordered after the halo.
@@ -222,6 +223,7 @@ SweepArgs sweep_args(df_handle *h)
     a.yunroll = h->yunroll;
     a.ywindow = h->ywindow;
     a.ycoop = h->ycoop;
+    a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
     a.ynt_stores = h->ynt_stores;
@@ -1562,6 +1564,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "zsplit") h->zsplit = value != 0;
     else if (k == "ycoop") {
         if (value < 0 || value > 3)
             return fail(DF_EINVAL, "ycoop must be 0 or 1, 2, 3 (16, 8, 4 taps per wave per chunk)");

@@ -1197,14 +1197,17 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 // x[col+1+i]. With N even, pairs P_m = (x[col-N+2m], x[col-N+2m+1]) are 16-B
 // aligned: even tap -N+2m uses P_m, odd tap -N+2m+1 uses (P_m.y, P_{m+1}.x), so
 // one 16-B noise load serves two taps and the order i = -N..N is unchanged.
-template <bool TABLE, bool NT, int ZU, bool PC>
+// SPLIT (packed planes with few tiles per SIMD; SweepArgs::zsplit): one 3-wave block per tile, wave c
+// sums component c's taps, the three sums meet in LDS and wave 0 runs the epilogue - three times the
+// waves in flight for the same bytes. Same sums, same epilogue: bit-identical.
+template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
-    const int tile = uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int tile = SPLIT ? (int)blockIdx.x : uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int Ny = a.Ny;
-    if (tile >= a.nstrips * Ny) return;
+    if (tile >= a.nstrips * Ny) return; // block-uniform when SPLIT
     int j = tile / a.nstrips;
     const int s = tile - j * a.nstrips;
     if (a.heavy_first) j = Ny - 1 - j;
@@ -1238,13 +1241,17 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             __syncthreads();
         }
     }
-    if (col >= a.Nz_loc) return; // padding lanes (after their share of the staging copy)
+    // padding lanes leave (after their share of the staging copy); SPLIT keeps them to the barrier
+    // (their loads stay inside the padded strip: B holds 128 cells per strip, r_zs Pz + 2 Nzp columns)
+    if (!SPLIT && col >= a.Nz_loc) return;
+    const int wv = uniform(threadIdx.x >> 6);
 
     double f0[3], f1[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         f0[c] = f1[c] = 0.0;
         if (!((a.comps_mask >> c) & 1)) continue;
+        if (SPLIT && c != wv) continue;
         const int N = a.Nz_st[c][(size_t)s * Ny + j];
         const double2 *gxp = reinterpret_cast<const double2 *>(a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + col - N);
         const double *bp = TABLE ? nullptr : a.Bz[c] + a.bzoff[c][(size_t)s * Ny + j] + 2 * lane; // tap t = i + N
@@ -1332,6 +1339,23 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             taps((lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane), f0[c], f1[c]);
         } else {
             taps(gxp, f0[c], f1[c]);
+        }
+    }
+
+    if constexpr (SPLIT) {
+        __shared__ double2 zsplit_part[3][64];
+        double2 mine = make_double2(0.0, 0.0);
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            if (c == wv) mine = make_double2(f0[c], f1[c]);
+        zsplit_part[wv][lane] = mine;
+        __syncthreads();
+        if (wv != 0) return;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const double2 v = zsplit_part[c][lane];
+            f0[c] = v.x;
+            f1[c] = v.y;
         }
     }
 
@@ -1424,6 +1448,10 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
         const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
         if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
+    } else if (a.zsplit) { // packed, one 3-wave block per tile
+        const unsigned b3 = (unsigned)tiles;
+        if (a.nt_loads) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<false, false, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
     } else if (a.nt_loads) {
         if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);

@@ -99,6 +99,7 @@ struct SweepArgs {
     int nt_stores;          // z-pass outputs stored non-temporally
     int ynt_stores;         // y-pass output (r_zs) stored non-temporally
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
+    int zsplit;             // packed z-pass: one 3-wave block per tile, a wave per component (few tiles per SIMD)
     int ycoop;              // packed y-pass: one block per (strip, row) tile, taps shared by 4 waves (long chains)
     int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)

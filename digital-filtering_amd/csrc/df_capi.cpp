@@ -639,7 +639,12 @@ int plan_strips(df_handle *h)
         // Long chains, packed: one block per tile, 8 taps per wave per chunk (the reference's grid: y-pass
         // 0.209 -> 0.181 ms, call -9%; profiles/r2/ab_ycoop_native.jsonl). c3-class planes lose with it.
         if (h->coeff_mode == DF_COEFF_PACKED && long_chain) h->ycoop = 2;
+        // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
+        // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
+        // profiles/r2/ab_zsplit.jsonl)
+        if (h->coeff_mode == DF_COEFF_PACKED && (long long)h->nstrips * s.Ny < 1024) h->zsplit = 1;
     }
+    if (const char *e = std::getenv("DFAMD_ZSPLIT")) h->zsplit = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {

@@ -189,17 +189,27 @@ class Ctx:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.device = self.local_rank
+        # DFAMD_EMULATE_HOSTS=1: a rehearsal of the N-GPU path on one GPU. Every rank uses device 0 and
+        # names its own host to RCCL (NCCL_HOSTID), whose duplicate-GPU check is per host; the ranks then
+        # talk through RCCL's socket transport on the loopback interface instead of xGMI. Same product
+        # calls, different transport: for checking the multi-GPU path, never for a scaling number.
+        self.emulated = os.environ.get("DFAMD_EMULATE_HOSTS", "0") == "1" and self.world > 1
+        if self.emulated:
+            self.device = 0
+            os.environ.update(NCCL_HOSTID=f"dfamd-emulated-host-{self.rank}", NCCL_SOCKET_IFNAME="lo",
+                              NCCL_IB_DISABLE="1", NCCL_NET="Socket")
         self.dist = None
 
     def init(self, torch, backend="nccl"):
         """backend "nccl" (RCCL, the bench) or "gloo" (CPU tests of this plumbing)."""
         self.torch = torch
         if backend == "nccl":
-            torch.cuda.set_device(self.local_rank)
+            torch.cuda.set_device(self.device)
         if self.world > 1:
             import torch.distributed as dist
             if backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", self.local_rank))
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.device))
             else:
                 dist.init_process_group("gloo")
             self.dist = dist
@@ -224,7 +234,7 @@ class Ctx:
 
 
 def make_filter(dfamd, ctx, wl, args, coeff_mode, split=True, comm_id=None):
-    kw = dict(seed=args.seed, device=ctx.local_rank, coeff_mode=coeff_mode, rows_per_wave=args.rows_per_wave)
+    kw = dict(seed=args.seed, device=ctx.device, coeff_mode=coeff_mode, rows_per_wave=args.rows_per_wave)
     if wl["plane"] == "native":
         return dfamd.DigitalFilter(plane="native", **kw)
     kw.update(plane="synthetic", Ny=wl["Ny"], Nz=wl["Nz"], N_min=wl["N_min"], N_max=wl["N_max"])
@@ -495,6 +505,7 @@ def main(argv=None):
                        "N_max": wl["N_max"], "dt": args.dt, "coeff_mode": args.coeff_mode,
                        "rows_per_wave": args.rows_per_wave,
                        "parallelism": f"z-strips x{ctx.world}" if ctx.world > 1 else "single GPU"},
+            "emulated_hosts": ctx.emulated or None,
             "parity_ok": parity["ok"] if parity else None,
             "rng_collective": "allgather" if (comm or {}).get("rng_collective") else "none",
             "phase_ms_per_call": head["phase_ms_per_call"],

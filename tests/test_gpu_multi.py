@@ -5,6 +5,12 @@ with rank +- 1 (df_capi.cpp phase_halo_rccl) and, with rng_replicate 0, the per-
 of accept counts and masks - then compares its strip with the whole plane run unsplit on its own
 GPU, bit for bit (fields, filt_old and the stream state). World 1 runs on any box (a one-rank
 communicator: the same init and calls, no peers); larger worlds are skipped below that many GPUs.
+
+Emulated hosts (any box with one GPU): every rank runs on device 0 and gets its own NCCL_HOSTID, so
+RCCL sees one GPU per "host" (its duplicate-GPU check compares bus ids within a host only) and
+connects the ranks through its socket transport over the loopback interface. The product's code is
+the same as on an 8-GPU node - the communicator init, the rank +- 1 grouped send/recv, the halo
+pack/unpack and the all-gather - only RCCL's transport underneath differs (socket, not xGMI).
 """
 import json
 import os
@@ -24,16 +30,24 @@ def n_gpus():
     return torch.cuda.device_count()  # does not initialise the GPU on this image
 
 
-def run_world(world, mode, replicate, Ny=256, Nz=1024, N_min=4, N_max=32, seed=11, dts=(1e-8, 1e-8, 1e-5)):
+def emulated_host_env(rank):
+    """Environment that makes RCCL treat this process as the only GPU of its own host."""
+    return dict(os.environ, NCCL_HOSTID=f"dfamd-emulated-host-{rank}", NCCL_SOCKET_IFNAME="lo",
+                NCCL_IB_DISABLE="1", NCCL_NET="Socket", HSA_ENABLE_IPC_MODE_LEGACY="0")
+
+
+def run_world(world, mode, replicate, Ny=256, Nz=1024, N_min=4, N_max=32, seed=11, dts=(1e-8, 1e-8, 1e-5),
+              emulate=False):
     sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
     import dfamd
-    cid = dfamd.comm_unique_id().hex()
+    cid = dfamd.comm_unique_id().hex()  # the bootstrap root lives in this process until the ranks join
     procs = []
     for r in range(world):
         spec = dict(rank=r, world=world, comm_id=cid, Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=seed,
-                    mode=mode, replicate=replicate, dts=list(dts))
+                    mode=mode, replicate=replicate, dts=list(dts), device=0 if emulate else r)
         procs.append(subprocess.Popen([sys.executable, WORKER, json.dumps(spec)], stdout=subprocess.PIPE,
-                                      stderr=subprocess.PIPE, text=True, start_new_session=True))
+                                      stderr=subprocess.PIPE, text=True, start_new_session=True,
+                                      env=emulated_host_env(r) if emulate else None))
     outs = []
     try:
         for p in procs:
@@ -54,8 +68,13 @@ def test_rccl_strips_match_unsplit_plane(world, mode, replicate):
     if n_gpus() < world:
         pytest.skip(f"needs {world} GPUs, box has {n_gpus()}")
     outs = run_world(world, mode, replicate)
+    check_world(outs, world, replicate)
+
+
+def check_world(outs, world, replicate, Nz=1024):
     cols = sorted(o["columns"] for o in outs)
-    assert cols[0][0] == 0 and cols[-1][1] == 1024
+    assert cols[0][0] == 0 and cols[-1][1] == Nz
+    assert all(a[1] == b[0] for a, b in zip(cols, cols[1:]))
     for o in outs:
         assert o["mismatch"] == {}, o
         assert o["rng_equal"], o
@@ -63,3 +82,13 @@ def test_rccl_strips_match_unsplit_plane(world, mode, replicate):
         assert c["rccl_ranks"] == world
         assert c["rng_collective"] == (0 if replicate else 1)
         assert c["halo_peers"] == (0 if world == 1 else (1 if o["rank"] in (0, world - 1) else 2))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 1), ("table", 0)])
+def test_rccl_strips_emulated_hosts(world, mode, replicate):
+    """world ranks on one GPU, one emulated host each: the peer send/recv path on a one-GPU box."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(world, mode, replicate, emulate=True)
+    check_world(outs, world, replicate)

@@ -67,6 +67,7 @@ struct CompDev {
     double *filt_old = nullptr, *fluc = nullptr, *filt = nullptr;
     long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
     long long by_size = 0, bz_size = 0;   // reference offset-packed sizes (this strip's cells)
+    int ycoop2_xcd[9] = {};               // row-pair y-pass tiles of XCD x: [ycoop2_xcd[x], ycoop2_xcd[x+1])
     double sa = 0, s1a = 0;
 };
 
@@ -101,6 +102,8 @@ struct df_handle {
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
+    int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
+    std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
     // z-strips: every rank counts every attempt block, so the halo send/recv is the call's only
     // collective (SURVEY 8e option B, north star "single RCCL halo exchange"). 0 = split counting
     // plus a per-call all-gather of counts and accept masks (option A), ordered after the halo.
@@ -223,6 +226,13 @@ SweepArgs sweep_args(df_handle *h)
     a.yunroll = h->yunroll;
     a.ywindow = h->ywindow;
     a.ycoop = h->ycoop;
+    a.ycoop2_run = 0;
+    for (int c = 0; c < 3; ++c)
+        for (int x = 0; x < 8; ++x) {
+            a.ycoop2_xcd[c][x] = h->c[c].ycoop2_xcd[x];
+            a.ycoop2_run = std::max(a.ycoop2_run, h->c[c].ycoop2_xcd[x + 1] - h->c[c].ycoop2_xcd[x]);
+        }
+    for (int c = 0; c < 3; ++c) a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -606,6 +616,38 @@ int read_config(df_handle *h, const df_config_c *cfg)
     return DF_OK;
 }
 
+// Row-pair y-pass tiles split into 8 contiguous runs of equal cost, one run per XCD (ypass_coop2_kernel):
+// a plain 1/8 split of the tile list hands XCDs whole runs of narrow-stencil rows or of a narrow last
+// strip (the reference's grid: N_y 28-212 along the rows, a 16-column last strip) and leaves them idle
+// while the others stream. Cost of a tile = its coefficient taps x live columns + ycoop_ovh full-strip
+// taps (a per-block fixed cost).
+void balance_ycoop2(df_handle *h, int c)
+{
+    constexpr int RR = 2; // rows per block of the row-pair y-pass
+    const int Ny = h->Ny, nrb = (Ny + RR - 1) / RR;
+    const std::vector<int> &Nst = h->y_nst[c];
+    std::vector<double> wgt((size_t)h->nstrips * nrb);
+    const double ovh = (double)h->ycoop_ovh * kStrip;
+    double tot = 0;
+    for (int st = 0; st < h->nstrips; ++st) {
+        const int live = std::min(kStrip, h->Nz_loc - st * kStrip);
+        for (int rb = 0; rb < nrb; ++rb) {
+            double taps = 0;
+            for (int j = rb * RR; j < std::min(Ny, rb * RR + RR); ++j) taps += 2 * Nst[(size_t)st * Ny + j] + 1;
+            tot += wgt[(size_t)st * nrb + rb] = taps * live + ovh;
+        }
+    }
+    int *xr = h->c[c].ycoop2_xcd;
+    int x = 1;
+    double acc = 0;
+    xr[0] = 0;
+    for (size_t t = 0; t < wgt.size() && x < 8; ++t) {
+        acc += wgt[t];
+        while (x < 8 && acc >= tot * x / 8) xr[x++] = (int)t + 1;
+    }
+    while (x <= 8) xr[x++] = (int)wgt.size();
+}
+
 // This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
 int plan_strips(df_handle *h)
 {
@@ -636,9 +678,11 @@ int plan_strips(df_handle *h)
             h->rows_per_wave = 1;
             if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
         } else h->rows_per_wave = 2;
-        // Long chains, packed: one block per tile, 8 taps per wave per chunk (the reference's grid: y-pass
-        // 0.209 -> 0.181 ms, call -9%; profiles/r2/ab_ycoop_native.jsonl). c3-class planes lose with it.
-        if (h->coeff_mode == DF_COEFF_PACKED && long_chain) h->ycoop = 2;
+        // Long chains, packed: one block per row pair, noise loads shared by both rows, the next chunk in
+        // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
+        // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
+        // c3-class planes lose with it.
+        if (h->coeff_mode == DF_COEFF_PACKED && long_chain) h->ycoop = 7;
         // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
         // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
         // profiles/r2/ab_zsplit.jsonl)
@@ -860,6 +904,8 @@ int alloc_components(df_handle *h)
                     Nst[dir][(size_t)st * Ny + j] = m;
                 }
         }
+        h->y_nst[c] = Nst[0]; // host copy for the row-block y-pass's XCD balance
+        balance_ycoop2(h, c);
         if ((rc = dalloc_t(h, &d.Ny_st, Nst[0].size()))) return rc;
         if ((rc = dalloc_t(h, &d.Nz_st, Nst[1].size()))) return rc;
         if ((rc = upload(h, d.Ny_st, Nst[0].data(), Nst[0].size()))) return rc;
@@ -1570,9 +1616,16 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
+    else if (k == "ycoop_ovh") {
+        if (value < 0) return fail(DF_EINVAL, "ycoop_ovh must be >= 0");
+        h->ycoop_ovh = value;
+        for (int c = 0; c < 3; ++c) balance_ycoop2(h, c);
+    }
     else if (k == "ycoop") {
-        if (value < 0 || value > 3)
-            return fail(DF_EINVAL, "ycoop must be 0 or 1, 2, 3 (16, 8, 4 taps per wave per chunk)");
+        if (value < 0 || value > 8 || value == 5 || value == 6)
+            return fail(DF_EINVAL, "ycoop must be 0 or 1, 2, 3 (16, 8, 4 taps per wave per chunk), "
+                                   "4 (8 with the next chunk's loads in flight), "
+                                   "7, 8 (row pairs, 4 or 8 noise rows per wave per chunk)");
         h->ycoop = value;
     }
     else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter

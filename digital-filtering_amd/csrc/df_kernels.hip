@@ -1084,7 +1084,9 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 // Every product and every addition is the one the per-wave kernel performs, in the same order
 // i = -N..N: bit-identical. On the reference's own grid (N_y up to 212, ~6 tiles per SIMD) a wave's
 // serial chain of 2N+1 dependent load rounds, not HBM bandwidth, set the per-wave kernel's time.
-template <bool NT, int KPW>
+// PIPE: the next chunk's loads are issued as soon as this chunk's products are in LDS, so they are in
+// flight through the barrier and the tap-order sum instead of after it (the barrier waits on LDS only).
+template <bool NT, int KPW, bool PIPE = false>
 __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
 {
     constexpr int CH = 4 * KPW; // taps per chunk
@@ -1108,8 +1110,8 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
     const double *bp = a.By[c] + a.byoff[c][(size_t)s * Ny + j] + 2 * lane;       // tap t at bp + t*128
     const double *np = a.ry[c] + (size_t)(j + a.Nyp[c] - N) * a.Pz + col;          // tap t at np + t*Pz
     double acc = 0.0; // thread k < 128: cell s*128 + k
-    for (int t0 = 0; t0 < T; t0 += CH) {
-        double2 b[KPW], n[KPW];
+    double2 b[KPW], n[KPW];
+    auto load = [&](int t0) {
 #pragma unroll
         for (int k = 0; k < KPW; ++k) {
             const int t = t0 + w + 4 * k;
@@ -1120,13 +1122,22 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
                 b[k] = n[k] = make_double2(0.0, 0.0);
             }
         }
+    };
+    if (PIPE) load(0);
+    for (int t0 = 0; t0 < T; t0 += CH) {
+        if (!PIPE) load(t0);
 #pragma unroll
         for (int k = 0; k < KPW; ++k) prod[w + 4 * k][lane] = make_double2(b[k].x * n[k].x, b[k].y * n[k].y);
+        if (PIPE && t0 + CH < T) load(t0 + CH); // block-uniform condition
         __syncthreads();
         if (threadIdx.x < kStrip) {
             const double *pc = reinterpret_cast<const double *>(&prod[0][0]) + threadIdx.x;
+#if defined(DF_ABLATE_COOPSUM)
+            acc += pc[0]; // timing only: one product per chunk
+#else
             const int nt = min(CH, T - t0);
             for (int u = 0; u < nt; ++u) acc += pc[u * kStrip];
+#endif
         }
         __syncthreads();
     }
@@ -1135,6 +1146,118 @@ __global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
         double *o = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + k;
         if (a.ynt_stores) __builtin_nontemporal_store(acc, o);
         else *o = acc;
+    }
+}
+
+// K4, block-cooperative form over a PAIR of rows (SweepArgs::ycoop 7, 8; 7 is the default for long
+// chains): one block per (strip, rows j0, j0 + 1). The block walks the union of the two rows' noise
+// ranges in chunks; wave w loads noise rows w, w+4, ... of the chunk once and both rows' coefficients
+// for them, so each noise load serves two products (the one-row form re-reads every noise row once per
+// output row: half its vector-memory bytes are noise). Threads 0-127 add row j0's products and threads
+// 128-255 row j0 + 1's, each over its own row's taps in the order i = -N..N: bit-identical to the other
+// forms. The next chunk's loads are in flight through the barrier and the sums (as PIPE).
+// Measured on the reference's grid (profiles/r2/ab_ycoop2_native.jsonl): y-pass 0.178 (one row, PIPE)
+// -> 0.157 ms; four rows per block, two chunks in flight and 8 noise rows per wave were slower.
+// A strip with fewer live columns than 128 (the last strip of a plane whose width is not a multiple
+// of 128: 16 of 128 on the reference's grid) folds G = 64 / P tap groups into the wave, P = live
+// column pairs rounded up to a power of two: lane l loads column pair l % P of noise row l / P, so one
+// load instruction covers G noise rows and the block walks its chain in 1/G of the chunks.
+// Blocks x, x+8, ... (one XCD) run tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]): contiguous runs of equal
+// coefficient bytes (balance_ycoop2 in df_capi.cpp).
+template <bool NT, int KPW>
+__global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
+{
+    constexpr int CH = 4 * KPW; // noise rows per chunk and tap group
+    constexpr int RR = 2, RH = 1; // rows per block, rows summed per thread
+    __shared__ double2 prod[RR * CH * 64];
+    const int c = blockIdx.y;
+    if (!((a.comps_mask >> c) & 1)) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int Ny = a.Ny, nrowblk = (Ny + RR - 1) / RR;
+    const int x = blockIdx.x & 7;
+    const int tile = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
+    if (tile >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
+    const int s = tile / nrowblk;             // rows ascending within a strip (L2 reuse of noise rows)
+    const int j0 = (tile - s * nrowblk) * RR;
+    const int nr = min(RR, Ny - j0);
+    // live column pairs of this strip -> P lanes per tap group (power of two), G groups per wave
+    const int pairs = min(kStrip / 2, (a.Nz_loc - s * kStrip + 1) >> 1);
+    int lp = 0;
+    while ((1 << lp) < pairs) ++lp;
+    const int P = 1 << lp, G = 64 >> lp, CHG = CH * G;
+    const int q = lane >> lp, p = lane & (P - 1);
+    int lo[RR], hi[RR]; // row r's noise rows [lo, hi] = j0 + r + [-N, N]
+    const double *bp[RR];
+    int mlo = 1 << 30, mhi = -(1 << 30);
+#pragma unroll
+    for (int r = 0; r < RR; ++r) {
+        const int rr = r < nr ? r : 0; // a missing row mirrors the first and is never summed
+        const int N = a.Ny_st[c][(size_t)s * Ny + j0 + rr];
+        lo[r] = j0 + rr - N;
+        hi[r] = j0 + rr + N;
+        mlo = min(mlo, lo[r]);
+        mhi = max(mhi, hi[r]);
+        bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + rr] + 2 * p; // tap t at bp + t*128
+    }
+    const int M = mhi - mlo + 1;
+    const int col = s * kStrip + 2 * p;
+    const bool live = col < a.Nz_loc;
+    const double *np = a.ry[c] + (size_t)(mlo + a.Nyp[c]) * a.Pz + col; // noise row mlo + u at np + u*Pz
+    double2 b[RR][KPW], n[KPW];
+    auto load = [&](int u0) {
+#pragma unroll
+        for (int k = 0; k < KPW; ++k) {
+            const int u = u0 + (w + 4 * k) * G + q, m = mlo + u;
+            n[k] = (live && u < M) ? DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)u * a.Pz), u)
+                                      : make_double2(0.0, 0.0);
+#pragma unroll
+            for (int r = 0; r < RR; ++r)
+                b[r][k] = (live && u < M && m >= lo[r] && m <= hi[r])
+                                 ? ldB<NT>(bp[r] + (ptrdiff_t)(m - lo[r]) * kStrip)
+                                 : make_double2(0.0, 0.0);
+        }
+    };
+    // row r, chunk slot v (noise row u0 + v), column pair p at prod[r*CH*64 + v*P + p]
+    const int rs = threadIdx.x >> 7, cell = threadIdx.x & (kStrip - 1); // summing thread: rows rs + 2i, cell
+    int lor[RH], hir[RH];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) { // selects: no indexed register array
+        lor[i] = rs ? lo[2 * i + 1] : lo[2 * i];
+        hir[i] = rs ? hi[2 * i + 1] : hi[2 * i];
+    }
+    double acc[RH];
+#pragma unroll
+    for (int i = 0; i < RH; ++i) acc[i] = 0.0;
+    load(0);
+    for (int u0 = 0; u0 < M; u0 += CHG) {
+#pragma unroll
+        for (int k = 0; k < KPW; ++k)
+#pragma unroll
+            for (int r = 0; r < RR; ++r)
+                prod[r * CH * 64 + ((w + 4 * k) * G + q) * P + p] =
+                    make_double2(b[r][k].x * n[k].x, b[r][k].y * n[k].y);
+        if (u0 + CHG < M) load(u0 + CHG); // block-uniform
+        __syncthreads();
+        if (cell < 2 * P) {
+#pragma unroll
+            for (int i = 0; i < RH; ++i) {
+                // this chunk's noise rows of row 2i + rs: u in [ua, ub) (wave-uniform)
+                const int ua = max(0, lor[i] - mlo - u0), ub = min(CHG, hir[i] - mlo - u0 + 1);
+                const double *pc = reinterpret_cast<const double *>(prod + (2 * i + rs) * CH * 64) + cell;
+                for (int u = ua; u < ub; ++u) acc[i] += pc[u * 2 * P];
+            }
+        }
+        __syncthreads();
+    }
+    const int k = s * kStrip + cell;
+#pragma unroll
+    for (int i = 0; i < RH; ++i) {
+        const int r = 2 * i + rs;
+        if (r < nr && cell < 2 * P && k < a.Nz_loc) {
+            double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + k;
+            if (a.ynt_stores) __builtin_nontemporal_store(acc[i], o);
+            else *o = acc[i];
+        }
     }
 }
 
@@ -1166,12 +1289,28 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
+    if (!table && a.ycoop >= 7) { // row pairs: 7 = 4 noise rows per wave per chunk (32 KiB LDS), 8 = 8 (64 KiB)
+        const dim3 grid((unsigned)(8 * a.ycoop2_run), 3);
+        if (a.ycoop == 7) {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop2_kernel<true, 4>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop2_kernel<false, 4>), grid, dim3(256), 0, st, a);
+        } else {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop2_kernel<true, 8>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop2_kernel<false, 8>), grid, dim3(256), 0, st, a);
+        }
+        return hipGetLastError();
+    }
     if (!table && a.ycoop) {
         const long long tiles = (long long)a.nstrips * a.Ny;
         const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);
         // ycoop 1: 16 taps per wave per chunk (64 KiB of LDS, 2 blocks per CU); 2: 8 taps (32 KiB, 4 blocks);
         // 3: 4 taps (16 KiB, 8 blocks)
-        if (a.ycoop >= 3) {
+        // 4: 8 taps with the next chunk's loads in flight through the sum (PIPE; 5 and 6, the 4- and
+        // 16-tap forms, were measured slower and removed)
+        if (a.ycoop == 4) {
+            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 8, true>), grid, dim3(256), 0, st, a);
+            else hipLaunchKernelGGL((ypass_coop_kernel<false, 8, true>), grid, dim3(256), 0, st, a);
+        } else if (a.ycoop >= 3) {
             if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 4>), grid, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((ypass_coop_kernel<false, 4>), grid, dim3(256), 0, st, a);
         } else if (a.ycoop == 2) {

@@ -101,6 +101,8 @@ struct SweepArgs {
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
     int zsplit;             // packed z-pass: one 3-wave block per tile, a wave per component (few tiles per SIMD)
     int ycoop;              // packed y-pass: one block per (strip, row) tile, taps shared by 4 waves (long chains)
+    int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)
+    int ycoop2_run;         // the longest such run (grid = 8 x this)
     int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is

@@ -136,6 +136,8 @@ def test_golden_synthetic(name):
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8, ycoop=0)),
                                          ("packed", dict(ycoop=1)), ("packed", dict(ycoop=3)), ("packed", dict(zsplit=1)),
+                                         ("packed", dict(ycoop=4)), ("packed", dict(ycoop=2)),
+                                         ("packed", dict(ycoop=8)), ("packed", dict(ycoop=7, ycoop_ovh=64)),
                                          ("table", dict(yunroll=8)),
                                          ("table", dict(gen_compact=0))])
 def test_golden_native_grid(mode, tuning):
@@ -223,7 +225,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(gen_split=16), dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256),
                 dict(ywin_T=0, zwin_T=4096, zwin_W=0), dict(ycoop=1), dict(gen_compact=0, ycoop=0),
                 dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0), dict(zsplit=1),
-                dict(zsplit=1, nt_loads=0), dict(zsplit=0)]
+                dict(zsplit=1, nt_loads=0), dict(zsplit=0), dict(ycoop=4), dict(ycoop=4, nt_loads=0),
+                dict(ycoop=7), dict(ycoop=8, nt_loads=0), dict(ycoop=7, ycoop_ovh=64), dict(ycoop_ovh=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

@@ -100,6 +100,9 @@ struct df_handle {
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
     int zstage = 1;    // table z-pass noise staged in LDS
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
+    // table y-pass: noise and coefficients loaded a whole 4-tap group ahead (ypass_kernel): c3 y-pass
+    // 0.141 -> 0.133 ms alone, the reference's grid and c2 -4.5% per call (profiles/r2/ab_ydeep_table.jsonl)
+    int ydeep = 1;
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
@@ -225,6 +228,7 @@ SweepArgs sweep_args(df_handle *h)
     a.heavy_first = h->heavy_first;
     a.yunroll = h->yunroll;
     a.ywindow = h->ywindow;
+    a.ydeep = h->ydeep;
     a.ycoop = h->ycoop;
     a.ycoop2_run = 0;
     for (int c = 0; c < 3; ++c)
@@ -1615,6 +1619,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "ydeep") h->ydeep = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
     else if (k == "ycoop_ovh") {
         if (value < 0) return fail(DF_EINVAL, "ycoop_ovh must be >= 0");

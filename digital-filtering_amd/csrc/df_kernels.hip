@@ -968,6 +968,52 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
+    if (TABLE && !PC && YU < 4 && a.ydeep && t + 7 <= bh) {
+        // Table mode, deep pipeline (SweepArgs::ydeep): taps go in groups of 4 noise rows; the next
+        // group's noise (4 x 16 B per lane) and coefficients (R x 4 scalars) are loaded a whole group
+        // ahead, so every load has a full group of taps (16 R mul/add pairs) between issue and use.
+        // Same products, same order: bit-identical.
+        double2 nA[4], nB[4];
+        double cA[R][4], cB[R][4];
+        auto ld = [&](int t0, double2 (&nn)[4], double (&cc)[R][4]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) nn[u] = noise(t0 + u);
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) cc[r][u] = DF_TCOEF(tb[r][t0 + u - r]);
+        };
+        auto taps = [&](const double2 (&nn)[4], const double (&cc)[R][4]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc0[r] += cc[r][u] * nn[u].x;
+                    acc1[r] += cc[r][u] * nn[u].y;
+                }
+        };
+        ld(t, nA, cA);
+        for (; t + 11 <= bh; t += 8) {
+            // sched_barrier: keep the compiler from sinking the next group's loads into the taps
+            ld(t + 4, nB, cB);
+            __builtin_amdgcn_sched_barrier(0);
+            taps(nA, cA);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(t + 8, nA, cA);
+            __builtin_amdgcn_sched_barrier(0);
+            taps(nB, cB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (t + 7 <= bh) { // one more full group pair: A holds t..t+3
+            ld(t + 4, nB, cB);
+            taps(nA, cA);
+            taps(nB, cB);
+            t += 8;
+        } else {
+            taps(nA, cA);
+            t += 4;
+        }
+    }
 #if !defined(DF_YPASS_NOWINDOW)
     if (TABLE && !PC && YU < 4 && Nlo == Nhi && a.ywindow && t + 5 <= bh) {
         // Table mode, one N for the whole tile (every tile of a row-uniform plane except where N

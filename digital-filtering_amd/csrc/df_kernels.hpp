@@ -104,6 +104,7 @@ struct SweepArgs {
     int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)
     int ycoop2_run;         // the longest such run (grid = 8 x this)
     int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
+    int ydeep;              // table y-pass: noise and coefficients loaded a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is
     // in the first W ticks of a T-tick period, so the CUs write together and the read stream runs

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Table z-pass with loads a whole 8-tap group ahead (zdeep) and the y-pass ydeep: parity, then A/B on c3 table.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r2y}
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+  -p no:cacheprovider -k "runtime_tuning or native_grid or bitexact" > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for t in "zdeep=0 zdeep=1" "ydeep=0,zdeep=0 ydeep=1,zdeep=1"; do
+  set -- $t
+  timeout -k 10 300 python tools/ab.py --a DFAMD_RNG_OVERLAP=0 --tune-a $1 --tune-b $2 --config c3 --mode table --rounds 9 --calls 20 >> $O/ab.jsonl 2>> $O/ab.err \
+    || { echo "ab failed"; tail -20 $O/ab.err; exit 1; }
+done
+for cfg in c3 native c2; do
+  timeout -k 10 300 python tools/ab.py --tune-a ydeep=0,zdeep=0 --tune-b ydeep=1,zdeep=1 --config $cfg --mode table --rounds 9 --calls 40 >> $O/ab.jsonl 2>> $O/ab.err
+done
+python3 -c "
+import json
+for l in open('$O/ab.jsonl'):
+    d=json.loads(l); a=d['A_median_ms']; b=d['B_median_ms']; print(d['config'], d['mode'], d['A'], a['ypass_ms'], a['zpass_ms'], a['wall_ms'], '|', d['B'], b['ypass_ms'], b['zpass_ms'], b['wall_ms'])"

@@ -8,6 +8,8 @@
 //   cpp-test rms seed             native grid, seeded, get_rms() -> ../files/cpp_vel_fluc_rms.csv
 //   cpp-test writers seed dt steps out   native grid, steps x filter(dt), then write_tecplot(out) and
 //                                 plot_RST_lerp() -> ../files/myRST.csv, ../files/duanRST.csv
+//   cpp-test twin Ny Nz Nmin Nmax seed steps csvA csvB   two objects on the process's one stream
+//                                 (df.cpp:334-335): A then B constructed, filter calls alternating
 #include "df.hpp"
 
 #include <cstdlib>
@@ -28,6 +30,26 @@ int main(int argc, char **argv)
         const int steps = std::atoi(argv[7]);
         for (int s = 0; s < steps; ++s) df.filter(1e-8);
         df.write_csv(argc > 8 ? argv[8] : "cpp_vel_fluc.csv");
+        return 0;
+    }
+
+    if (argc >= 10 && std::string(argv[1]) == "twin") {
+        config.plane = DF_PLANE_SYNTHETIC;
+        config.Ny = std::atoi(argv[2]);
+        config.Nz = std::atoi(argv[3]);
+        config.N_min = std::atoi(argv[4]);
+        config.N_max = std::atoi(argv[5]);
+        config.seed = std::strtoull(argv[6], nullptr, 10);
+        config.seed_from_random_device = false;
+        DIGITAL_FILTER a(config);
+        DIGITAL_FILTER b(config); // continues the stream a's step 0 left (the reference's statics)
+        const int steps = std::atoi(argv[7]);
+        for (int s = 0; s < steps; ++s) {
+            a.filter(1e-8);
+            b.filter(1e-8);
+        }
+        a.write_csv(argv[8]);
+        b.write_csv(argv[9]);
         return 0;
     }
 

@@ -13,10 +13,11 @@
 // Deliberate differences: DFConfig fields are honoured
 // (the reference ignores them; their defaults here are its hard-coded values);
 // input paths come from the config instead of "../files/RST.dat" / "../line.dat";
-// filter() writes its CSV only when DFConfig::csv_path is set; the RNG stream
-// is per object (seeded like the reference when seed_from_random_device) instead
-// of one function-local static shared by every object; errors throw
-// std::runtime_error instead of printing to cerr and continuing.
+// filter() writes its CSV only when DFConfig::csv_path is set; errors throw
+// std::runtime_error instead of printing to cerr and continuing. The RNG stream is
+// the reference's: one process-wide stream shared by every object in call order
+// (df.cpp:334-335's function-local statics; DFConfig::shared_stream, the default),
+// or per object with shared_stream = false.
 #pragma once
 
 #include "df_c.h"
@@ -66,6 +67,25 @@ struct DFCheckpoint {
     Vector filt_old_u, filt_old_v, filt_old_w;
 };
 
+// The reference draws every object's noise from ONE pcg32 + normal_distribution, function-local
+// statics of generate_white_noise (df.cpp:334-335): the first object to draw seeds it, later objects
+// continue it in call order (constructor step 0 included). Each handle here owns a device-side copy
+// of the stream; with DFConfig::shared_stream the objects of a process hand this one state on: an
+// object that draws after another first loads the shared state into its handle (df_set_rng_state,
+// which regenerates the prefetched noise), and every draw publishes the state it leaves.
+struct DFSharedStream {
+    bool seeded = false;
+    std::uint64_t state = 0;
+    int saved_flag = 0;
+    double saved = 0.0;
+    const void *last = nullptr; // the object whose handle holds the current state
+};
+inline DFSharedStream &df_shared_stream()
+{
+    static DFSharedStream s; // one per process (inline function: one instance across translation units)
+    return s;
+}
+
 struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     double d_i = 0.0013, rho_e = 0.044, U_e = 869.1, mu_e = 7.1212e-6;
     int vel_file_offset = 0, vel_file_N_values = 0;
@@ -89,6 +109,7 @@ struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     int host_mirror = 1;         // 1: refresh u/v/w.fluc, filt_old, T', rho' after every call; 0: never
     int mirror_coefficients = -1; // by/bz host copies: 1 always, 0 never, -1 when <= 1 GiB
     bool verbose = true;         // print "Filtering took X seconds." (df.cpp:464)
+    bool shared_stream = true;   // one stream for every object of the process, as the reference's statics
     bool resume = false;         // start the stream at (rng_state, rng_saved_flag, rng_saved)
     std::uint64_t rng_state = 0;
     int rng_saved_flag = 0;
@@ -204,9 +225,17 @@ class DIGITAL_FILTER {
         c.rng_state = config.rng_state;
         c.rng_saved_flag = config.rng_saved_flag;
         c.rng_saved = config.rng_saved;
+        DFSharedStream &ss = df_shared_stream();
+        if (config.shared_stream && !config.resume && ss.seeded) { // step 0 continues the process's stream
+            c.rng_resume = 1;
+            c.rng_state = ss.state;
+            c.rng_saved_flag = ss.saved_flag;
+            c.rng_saved = ss.saved;
+        }
         h_ = df_create(&c);
         if (!h_) throw std::runtime_error(std::string("DIGITAL_FILTER: ") + df_last_error());
         try {
+            stream_out(); // step 0 drew from the stream
             mirror_setup();
         } catch (...) { // the destructor does not run for a half-built object
             df_destroy(h_);
@@ -216,9 +245,31 @@ class DIGITAL_FILTER {
     }
     DIGITAL_FILTER(const DIGITAL_FILTER &) = delete;
     DIGITAL_FILTER &operator=(const DIGITAL_FILTER &) = delete;
-    ~DIGITAL_FILTER() { df_destroy(h_); }
+    ~DIGITAL_FILTER()
+    {
+        DFSharedStream &ss = df_shared_stream();
+        if (ss.last == this) ss.last = nullptr; // the state stays published
+        df_destroy(h_);
+    }
 
   private:
+    // Shared stream (DFConfig::shared_stream): load the process's state before a draw unless this
+    // handle already holds it, publish the state after.
+    void stream_in()
+    {
+        DFSharedStream &ss = df_shared_stream();
+        if (!cfg_.shared_stream || !ss.seeded || ss.last == this) return;
+        check(df_set_rng_state(h_, ss.state, ss.saved_flag, ss.saved));
+        ss.last = this;
+    }
+    void stream_out()
+    {
+        if (!cfg_.shared_stream) return;
+        DFSharedStream &ss = df_shared_stream();
+        check(df_rng_state(h_, &ss.state, &ss.saved_flag, &ss.saved));
+        ss.seeded = true;
+        ss.last = this;
+    }
     // Host mirrors of the setup (rows, scalars, vertices, half-widths) and of step 0's fields.
     void mirror_setup()
     {
@@ -268,7 +319,12 @@ class DIGITAL_FILTER {
     void read_line_file() {}
 
     // ====== hot path (df.cpp:332-485), on the GPU
-    void generate_white_noise() { check(df_generate_white_noise(h_)); }
+    void generate_white_noise()
+    {
+        stream_in();
+        check(df_generate_white_noise(h_));
+        stream_out();
+    }
     void filtering_sweeps(FilterField &F)
     {
         const int c = comp_of(F);
@@ -294,10 +350,12 @@ class DIGITAL_FILTER {
     void filter(double dt_input)
     {
         dt = dt_input;
+        stream_in();
         auto start = NOW;
         check(df_filter(h_, dt));
         check(df_sync(h_));
         auto end = NOW;
+        stream_out();
         if (cfg_.verbose) {
             auto elapsed = std::chrono::duration<double>(end - start);
             std::cout << "Filtering took " << elapsed.count() << " seconds." << std::endl;
@@ -332,12 +390,14 @@ class DIGITAL_FILTER {
         check(df_rms_reset(h_));
         rms_counter = 0;
         dt = 1e-5; // df.cpp:594
+        stream_in();
         for (int i = 0; i < 500; ++i) {
             check(df_filter(h_, dt)); // noise, sweeps, correlate, RST, SRA (df.cpp:597-605)
             check(df_rms_add(h_));
             rms_counter++;
         }
         check(df_sync(h_));
+        stream_out();
         refresh();
         plot_rms();
     }
@@ -489,6 +549,7 @@ class DIGITAL_FILTER {
         for (const Vector *f : {&ck.filt_old_u, &ck.filt_old_v, &ck.filt_old_w})
             if ((int)f->size() != n_cells) throw std::invalid_argument("checkpoint is for another plane");
         check(df_set_rng_state(h_, ck.rng_state, ck.rng_saved_flag, ck.rng_saved));
+        stream_out(); // the restored state is the process's stream from here on
         check(df_set_field(h_, DF_FILT_OLD_U, ck.filt_old_u.data()));
         check(df_set_field(h_, DF_FILT_OLD_V, ck.filt_old_v.data()));
         check(df_set_field(h_, DF_FILT_OLD_W, ck.filt_old_w.data()));

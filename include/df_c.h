@@ -151,8 +151,9 @@ int df_get_comp_info(df_handle *h, int comp, int *Ny_max, int *Nz_max, long long
 /* Offset-packed coefficients exactly as FilterField::by / bz (df.cpp:151-216). */
 int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n);
 
-/* Process-wide RNG stream of the reference (df.cpp:334-335) is per handle here:
- * pcg32 state, normal_distribution cached flag and value. Synchronizes. */
+/* The reference's process-wide RNG stream (df.cpp:334-335) as each handle holds it: pcg32 state,
+ * normal_distribution cached flag and value. Synchronizes. include/df.hpp hands one state on between
+ * the objects of a process through these two calls (DFConfig::shared_stream). */
 int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved);
 int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved);
 /* Noise arrays as the reference holds them after the sweeps (FilterField r_ys /

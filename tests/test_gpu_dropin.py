@@ -75,6 +75,34 @@ def test_cpp_driver_filter_csv_matches_oracle(tmp_path):
     assert float(np.abs(A - B).max()) <= 1e-9 * max(1.0, float(np.abs(B).max()))
 
 
+def test_cpp_two_objects_share_the_process_stream(tmp_path):
+    # df.cpp:334-335: the pcg32 and normal_distribution are function-local statics, so a second
+    # DIGITAL_FILTER continues the stream of the first, in call order (DFConfig::shared_stream).
+    # The oracle keeps a pointer to its Rng: two oracle filters on one Rng are the reference's statics.
+    a_csv, b_csv = tmp_path / "a.csv", tmp_path / "b.csv"
+    out = subprocess.run([EXE, "twin", "40", "72", "2", "8", "23", "2", str(a_csv), str(b_csv)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    rng = O.Rng(seed=23)
+    oa = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=40, Nz=72, N_min=2, N_max=8, rng=rng)
+    ob = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=40, Nz=72, N_min=2, N_max=8, rng=rng)
+    for _ in range(2):
+        oa.filter(1e-8)
+        ob.filter(1e-8)
+    for csv, o, name in ((a_csv, oa, "oa.csv"), (b_csv, ob, "ob.csv")):
+        ref = tmp_path / name
+        o.write_csv(str(ref))
+        A = np.loadtxt(csv, delimiter=",", skiprows=1)
+        B = np.loadtxt(ref, delimiter=",", skiprows=1)
+        assert A.shape == B.shape == (40 * 72, 7)
+        assert np.array_equal(A[:, :2], B[:, :2])
+        assert float(np.abs(A - B).max()) <= 1e-9 * max(1.0, float(np.abs(B).max())), name
+    # the two objects drew different parts of the stream
+    A = np.loadtxt(a_csv, delimiter=",", skiprows=1)
+    B = np.loadtxt(b_csv, delimiter=",", skiprows=1)
+    assert float(np.abs(A[:, 2:] - B[:, 2:]).max()) > 0
+
+
 def test_variance_invariant_over_time():
     """sum b^2 = 1 and the variance-preserving correlation give
     Var(u') -> R11, Cov(u',v') -> R21, Var(v') -> R22, Var(w') -> R33 per row."""

@@ -370,7 +370,7 @@ def summarize(ctx, wl, args, recs):
         cm = recs[0]["comm"] or {}
         out["multi_gpu"] = {
             "rccl_ranks": cm.get("rccl_ranks"),
-            "rng_collective": ("allgather(counts, wave counts, accept masks)" if cm.get("rng_collective")
+            "rng_collective": ("allgather(block and wave accept counts; K3 recounts its waves' flags)" if cm.get("rng_collective")
                                else "none: every rank counts the whole stream (replicated), halo is the only collective"),
             "halo_ms_per_call": {"max": max(r["phase_ms_per_call"]["halo_ms"] for r in recs),
                                  "min": min(r["phase_ms_per_call"]["halo_ms"] for r in recs)},

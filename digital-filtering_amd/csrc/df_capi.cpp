@@ -107,9 +107,10 @@ struct df_handle {
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
-    // z-strips: every rank counts every attempt block, so the halo send/recv is the call's only
-    // collective (SURVEY 8e option B, north star "single RCCL halo exchange"). 0 = split counting
-    // plus a per-call all-gather of counts and accept masks (option A), ordered after the halo.
+    // z-strips: 1 = every rank counts every attempt block, so the halo send/recv is the call's only
+    // collective (SURVEY 8e option B, north star "single RCCL halo exchange"; the packed default).
+    // 0 = split counting plus a per-call all-gather of block and wave counts (option A), ordered after
+    // the halo; K3 recomputes the accept flags of the waves it runs (the table-mode default).
     int rng_replicate = 1;
     int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
@@ -325,6 +326,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     rs = h->overlap ? h->rng_stream : h->stream;
     HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
     g = h->geom;
+    g.recount = h->split_count ? 1 : 0;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
@@ -348,8 +350,8 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
     const int set = (int)(h->gen_launched & 1);
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
-    // every rank holds every block's accept masks (gathered with the counts), so K3 never
-    // redraws accept decisions
+    // split counting exchanges counts only: K3 recomputes the accept flags of the waves it runs
+    // (g.recount), a sixth or less of all waves on an interior rank of 8
     HIP_OR(launch_rng_finish(g, h->rstate + (h->gen_launched & 1), h->rstate + ((h->gen_launched + 1) & 1),
                              h->counts, h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks,
                              h->err_dev, h->rng_blocks, nb_scan, rs),
@@ -383,9 +385,6 @@ int launch_gen_group(std::vector<df_handle *> &hs)
             HIP_OR(hipMemcpyAsync(h->counts + at, hs[o]->counts + at, h->rng_chunk * sizeof(int), hipMemcpyDefault,
                                   rss[r]),
                    DF_EHIP);
-            HIP_OR(hipMemcpyAsync(h->masks + at * kRngThreads, hs[o]->masks + at * kRngThreads,
-                                  (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t), hipMemcpyDefault, rss[r]),
-                   DF_EHIP);
             HIP_OR(hipMemcpyAsync(h->wave_counts + at * kWavesPerBlock, hs[o]->wave_counts + at * kWavesPerBlock,
                                   (size_t)h->rng_chunk * kWavesPerBlock * sizeof(int), hipMemcpyDefault, rss[r]),
                    DF_EHIP);
@@ -408,11 +407,9 @@ int launch_gen(df_handle *h)
     if (rc) return rc;
     if (h->split_count) {
         int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
-        const size_t mbytes = (size_t)h->rng_chunk * kRngThreads * sizeof(uint16_t);
-        uint16_t *mmine = h->masks + (size_t)h->rank * h->rng_chunk * kRngThreads;
         const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
-        if (h->rng_comm) { // the RNG's one exchange: accept counts (block, wave) and masks
+        if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
             // Never concurrent with the halo send/recv of the other communicator: every rank issues
             // the all-gather only after its own halo group of the call just enqueued has completed,
             // so the two communicators' kernels run in the same order on every rank.
@@ -420,15 +417,11 @@ int launch_gen(df_handle *h)
             NCCL_OR(ncclGroupStart());
             NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
             NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
-            NCCL_OR(ncclAllGather(mmine, h->masks, mbytes, ncclUint8, h->rng_comm, rs));
             NCCL_OR(ncclGroupEnd());
         } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
             for (int o = 0; o < h->world; ++o)
                 if (o != h->rank) {
                     HIP_OR(hipMemcpyAsync(h->counts + (size_t)o * h->rng_chunk, mine, h->rng_chunk * sizeof(int),
-                                          hipMemcpyDeviceToDevice, rs),
-                           DF_EHIP);
-                    HIP_OR(hipMemcpyAsync(h->masks + (size_t)o * h->rng_chunk * kRngThreads, mmine, mbytes,
                                           hipMemcpyDeviceToDevice, rs),
                            DF_EHIP);
                     HIP_OR(hipMemcpyAsync(h->wave_counts + (size_t)o * nwc, wmine, nwc * sizeof(int),
@@ -611,6 +604,12 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GRAPH")) h->use_graph = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
+    // Table mode splits the counting (one small all-gather of counts beside the halo): its sweeps are
+    // VALU-bound like the RNG, so every rank counting the whole stream shows (one rank of a c4 split
+    // in 8: 0.28-0.30 -> 0.24-0.27 ms per call). Packed keeps the halo as the call's only collective:
+    // its sweeps are HBM-bound and hide the replicated count (equal within noise at N = 4, 8;
+    // profiles/r2/strip_timing_c4_counts_only.jsonl).
+    h->rng_replicate = h->coeff_mode == DF_COEFF_PACKED ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_RNG_REPLICATE")) h->rng_replicate = std::atoi(e) != 0;
     if (h->solo_strip && !h->rng_replicate) h->split_count = true;
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
@@ -1773,7 +1772,7 @@ int df_comm_info(df_handle *h, df_comm_stats *out)
     out->rng_collective = h->split_count && h->rng_comm ? 1 : 0;
     const long long others = (long long)h->rng_chunk * (h->world - 1);
     out->rng_bytes_received =
-        out->rng_collective ? others * (long long)(sizeof(int) + kWavesPerBlock * sizeof(int) + kRngThreads * sizeof(uint16_t)) : 0;
+        out->rng_collective ? others * (long long)(sizeof(int) + kWavesPerBlock * sizeof(int)) : 0;
     out->rng_blocks_counted = h->split_count ? h->rng_chunk : h->rng_blocks;
     out->rng_blocks_total = h->rng_blocks;
     return DF_OK;

@@ -112,24 +112,13 @@ __device__ __forceinline__ uint64_t thread_first_state(const RngGeom &g, uint64_
     return jt.mult * (jb.mult * S + jb.plus) + jt.plus;
 }
 
-// Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
-// the last z-strip rank's share) report zero.
-__global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                               int *__restrict__ counts, int *__restrict__ wave_counts,
-                                                               uint16_t *__restrict__ masks, int b0, int nb_total)
+// The accept flags of thread tid of attempt block gb (bit m: its attempt m), from the call's start state S.
+// The screen reads outputs 1 and 3 of each attempt only: the lane walks the states one and three steps
+// into its attempts directly, each with one 64-bit multiply-add per attempt (J s + P_k, the 256-step jump
+// conjugated: J and the step commute), instead of the attempt start plus two steps.
+__device__ __forceinline__ uint32_t lane_accept_bits(const RngGeom &g, uint64_t S, int gb, int tid)
 {
-    __shared__ int wsum[kRngThreads / 64];
-    const int tid = threadIdx.x, w = tid >> 6;
-    const int gb = b0 + blockIdx.x;
-    if (gb >= nb_total) {
-        if (tid == 0) counts[gb] = 0;
-        if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
-        return;
-    }
-    const uint64_t st0 = thread_first_state(g, sin->state, gb, tid);
-    // The screen reads outputs 1 and 3 of each attempt only: the lane walks the states one and three
-    // steps into its attempts directly, each with one 64-bit multiply-add per attempt (J s + P_k, the
-    // 256-step jump conjugated: J and the step commute), instead of the attempt start plus two steps.
+    const uint64_t st0 = thread_first_state(g, S, gb, tid);
     uint64_t s1 = st0 * kPcgMult + kPcgInc;
     uint64_t s3 = s1 * kPcgMult2 + kPcgInc2;
     uint32_t bits = 0, unsure = 0;
@@ -149,6 +138,24 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
         for (int k = 0; k < m; ++k) s = g.next_mult * s + g.next_plus;
         if (polar_attempt(s).accept) bits |= 1u << m;
     }
+    return bits;
+}
+
+// Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
+// the last z-strip rank's share) report zero.
+__global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                               int *__restrict__ counts, int *__restrict__ wave_counts,
+                                                               uint16_t *__restrict__ masks, int b0, int nb_total)
+{
+    __shared__ int wsum[kRngThreads / 64];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const int gb = b0 + blockIdx.x;
+    if (gb >= nb_total) {
+        if (tid == 0) counts[gb] = 0;
+        if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
+        return;
+    }
+    const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
     int cnt = __builtin_popcount(bits);
     masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -389,7 +396,8 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
     const int gw = uniform(tasks[slot].gw);
     long long rank_w = tasks[slot].r_lo; // uniform
     const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
-    const uint32_t bits = masks[(size_t)b * kRngThreads + tid];
+    // split counting: only counts were exchanged, so the flags of another rank's blocks are recomputed
+    const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
     uint64_t st = thread_first_state(g, sin->state, b, tid); // start of attempt m
@@ -647,7 +655,8 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     const int gw = uniform(tasks[slot].gw);
     long long rank_w = tasks[slot].r_lo; // uniform
     const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
-    const uint32_t bits = masks[(size_t)b * kRngThreads + tid];
+    // split counting: only counts were exchanged, so the flags of another rank's blocks are recomputed
+    const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
     uint64_t st = thread_first_state(g, sin->state, b, tid);

@@ -63,6 +63,7 @@ struct RngGeom {
     int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
                                    // iterations, so few-wave planes get short serial chains
     int gen_compact;               // K3 form: 1 = accepted attempts compacted into full batches (default), 0 = sequential
+    int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
     int fast_log;                  // 1: log_r2 (table-driven, df_rng.hpp) in the polar transform; 0: the device library's log
     const LogTabEntry *log_tab;    // kLogTab entries (build_log_table)
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)

@@ -23,8 +23,8 @@ def main():
     plane = dict(plane="synthetic", Ny=spec["Ny"], Nz=spec["Nz"], N_min=spec["N_min"], N_max=spec["N_max"],
                  seed=spec["seed"], coeff_mode=spec["mode"], device=spec.get("device", rank))
     h = dfamd.DigitalFilter(rank=rank, world=world, comm_id=bytes.fromhex(spec["comm_id"]), **plane)
-    if not spec.get("replicate", 1):
-        h.set_tuning("rng_replicate", 0)  # split counting: the per-call all-gather of counts and masks
+    if "replicate" in spec:  # 1: every rank counts the whole stream; 0: split counting + the counts all-gather
+        h.set_tuning("rng_replicate", int(spec["replicate"]))
     for dt in spec["dts"]:
         h.filter(dt)
     h.sync()

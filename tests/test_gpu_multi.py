@@ -2,7 +2,7 @@
 
 Each rank runs the product's peer path - ncclCommInitRank, the grouped ncclSend/ncclRecv halo
 with rank +- 1 (df_capi.cpp phase_halo_rccl) and, with rng_replicate 0, the per-call all-gather
-of accept counts and masks - then compares its strip with the whole plane run unsplit on its own
+of block and wave accept counts - then compares its strip with the whole plane run unsplit on its own
 GPU, bit for bit (fields, filt_old and the stream state). World 1 runs on any box (a one-rank
 communicator: the same init and calls, no peers); larger worlds are skipped below that many GPUs.
 
@@ -63,7 +63,7 @@ def run_world(world, mode, replicate, Ny=256, Nz=1024, N_min=4, N_max=32, seed=1
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 1), ("packed", 0)])
+@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 1), ("packed", 0), ("table", 0)])
 def test_rccl_strips_match_unsplit_plane(world, mode, replicate):
     if n_gpus() < world:
         pytest.skip(f"needs {world} GPUs, box has {n_gpus()}")

@@ -608,15 +608,15 @@ __device__ __forceinline__ void gen_batch(const RngGeom &g, const WaveDest &w, c
     const bool last = live && rank == A - 1;
     if (!(d0 || d1 || last)) return; // the whole batch leaves at once where nothing is stored here
     const uint64_t st = ring[(head + lane) & (kGenRing - 1)];
-    uint64_t s4 = st;
+    uint64_t s3 = st;
     PolarAttempt a;
     if (g.debug_flags & 4) {
         a.x = (double)(uint32_t)st * 1e-10;
         a.y = 0.5;
         a.r2 = 0.5;
-        s4 = st + 4;
+        s3 = st + 3;
     } else {
-        a = polar_attempt(s4); // the draws K1 tested
+        a = polar_draws(st, s3); // the draws K1 tested; the fourth step only for the call's last attempt
     }
     const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * (g.fast_log ? log_r2(a.r2, g.log_tab) : log(a.r2)) / a.r2);
     const double xm = a.x * mult;
@@ -632,7 +632,7 @@ __device__ __forceinline__ void gen_batch(const RngGeom &g, const WaveDest &w, c
         if (d1) *d1 = n1;
     }
     if (last) {
-        sout->state = s4; // state after this attempt's 4th output
+        sout->state = s3 * kPcgMult + kPcgInc; // state after this attempt's 4th output
         sout->saved_flag = (int)((g.Q - f) & 1u);
         sout->saved = xm;
     }

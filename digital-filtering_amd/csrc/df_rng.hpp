@@ -96,6 +96,30 @@ DF_HD PolarAttempt polar_attempt(uint64_t &state)
     return a;
 }
 
+// The same attempt from its first state without the fourth step: `s3` is left at the state of the
+// fourth output, so the state after the attempt is one more step (s3 * mult + inc), which only the
+// call's last attempt needs.
+DF_HD PolarAttempt polar_draws(uint64_t s, uint64_t &s3)
+{
+    uint32_t o[4];
+    o[0] = pcg_output(s);
+    s = s * kPcgMult + kPcgInc;
+    o[1] = pcg_output(s);
+    s = s * kPcgMult + kPcgInc;
+    o[2] = pcg_output(s);
+    s = s * kPcgMult + kPcgInc;
+    o[3] = pcg_output(s);
+    s3 = s;
+    PolarAttempt a;
+    a.x = 2.0 * canonical_from(o[0], o[1]) - 1.0;
+    a.y = 2.0 * canonical_from(o[2], o[3]) - 1.0;
+    double xx = a.x * a.x;
+    double yy = a.y * a.y;
+    a.r2 = xx + yy;
+    a.accept = !(a.r2 > 1.0 || a.r2 == 0.0);
+    return a;
+}
+
 // Two pcg32 steps at once: state -> mult2*state + inc2 (pcg_jump(2)).
 constexpr uint64_t kPcgMult2 = 0x685f98a2018fade9ULL;
 constexpr uint64_t kPcgInc2 = 0x1a08ee1184ba6d32ULL;

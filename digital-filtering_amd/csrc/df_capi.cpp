@@ -98,7 +98,9 @@ struct df_handle {
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
     int ynt_stores = 1; // the y-pass output likewise
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)
-    int zstage = 1;    // table z-pass noise staged in LDS
+    // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
+    // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
+    int zstage = 2;
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
     // table y-pass: noise and coefficients loaded a whole 4-tap group ahead (ypass_kernel): c3 y-pass
     // 0.141 -> 0.133 ms alone, the reference's grid and c2 -4.5% per call (profiles/r2/ab_ydeep_table.jsonl)
@@ -250,7 +252,7 @@ SweepArgs sweep_args(df_handle *h)
     int nzp = 0;
     for (int c = 0; c < 3; ++c) nzp = std::max(nzp, a.Nzp[c]);
     a.zstage_reg = 4 * kStrip + 2 * nzp;
-    a.zstage = h->zstage && 3 * a.zstage_reg * (int)sizeof(double) <= 64 * 1024;
+    a.zstage = 3 * a.zstage_reg * (int)sizeof(double) <= 64 * 1024 ? h->zstage : 0;
     return a;
 }
 
@@ -1616,7 +1618,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "nt_stores") h->nt_stores = h->ynt_stores = value != 0;
     else if (k == "znt_stores") h->nt_stores = value != 0;
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
-    else if (k == "zstage") h->zstage = value != 0;
+    else if (k == "zstage") h->zstage = value < 0 ? 0 : (value > 2 ? 2 : value);
     else if (k == "ywindow") h->ywindow = value != 0;
     else if (k == "ydeep") h->ydeep = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;

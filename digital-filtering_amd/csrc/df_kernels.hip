@@ -1394,6 +1394,55 @@ hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipSt
 // SPLIT (packed planes with few tiles per SIMD; SweepArgs::zsplit): one 3-wave block per tile, wave c
 // sums component c's taps, the three sums meet in LDS and wave 0 runs the epilogue - three times the
 // waves in flight for the same bytes. Same sums, same epilogue: bit-identical.
+// Table z-pass staging: row j's noise of strips [s0, s0 + ns) plus N columns either side, per
+// component, into LDS regions of a.zstage_reg doubles. zstage 2: 16-B copies with each thread's loads
+// (up to 3 per component) all issued before its LDS stores, so a block waits for one round trip
+// instead of one per element; rows start 16-B aligned (pitch, Nzp and N even), checked per block.
+__device__ __forceinline__ void zstage_copy(const SweepArgs &a, double *lds, int j, int s0, int ns, int nthr)
+{
+    const int tid = threadIdx.x;
+    const double *src[3];
+    int cnt[3];
+    bool vec = a.zstage >= 2;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        cnt[c] = 0;
+        src[c] = nullptr;
+        if (!((a.comps_mask >> c) & 1)) continue;
+        const int N = a.Nz_st[c][(size_t)s0 * a.Ny + j];
+        src[c] = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + s0 * kStrip - N;
+        cnt[c] = ns * kStrip + 2 * N;
+        vec = vec && ((uintptr_t)src[c] & 15) == 0 && (cnt[c] & 1) == 0;
+    }
+    if (!vec) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+            for (int e = tid; e < cnt[c]; e += nthr) lds[c * a.zstage_reg + e] = src[c][e];
+        return;
+    }
+    double2 v[3][3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int e = tid + k * nthr;
+            if (e < cnt[c] / 2) v[c][k] = reinterpret_cast<const double2 *>(src[c])[e];
+        }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        dvec2 *d = reinterpret_cast<dvec2 *>(lds + c * a.zstage_reg); // zstage_reg even: 16-B regions
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int e = tid + k * nthr;
+            if (e < cnt[c] / 2) d[e] = dvec2{v[c][k].x, v[c][k].y};
+        }
+        for (int e = tid + 3 * nthr; e < cnt[c] / 2; e += nthr) { // wide stencils: the rest
+            const double2 x = reinterpret_cast<const double2 *>(src[c])[e];
+            d[e] = dvec2{x.x, x.y};
+        }
+    }
+}
+
 template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
@@ -1424,14 +1473,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             staged = ns[Ny] == N0 && ns[2 * Ny] == N0 && ns[3 * Ny] == N0;
         }
         if (staged) {
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                if (!((a.comps_mask >> c) & 1)) continue;
-                const int N = a.Nz_st[c][(size_t)s0 * Ny + j];
-                const double *src = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + s0 * kStrip - N;
-                double *dst = zstage_lds + c * a.zstage_reg;
-                for (int e = threadIdx.x; e < 4 * kStrip + 2 * N; e += 256) dst[e] = src[e];
-            }
+            zstage_copy(a, zstage_lds, j, s0, 4, 256);
             __syncthreads();
         }
     }

@@ -99,7 +99,8 @@ struct SweepArgs {
     int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
     int nt_stores;          // z-pass outputs stored non-temporally
     int ynt_stores;         // y-pass output (r_zs) stored non-temporally
-    int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS
+    int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS (2: 16-B copy,
+                            // all loads issued before the stores)
     int zsplit;             // packed z-pass: one 3-wave block per tile, a wave per component (few tiles per SIMD)
     int ycoop;              // packed y-pass: one block per (strip, row) tile, taps shared by 4 waves (long chains)
     int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)

@@ -194,7 +194,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * 1 (default) = the table-driven log of the polar transform, 0 = the device math library's log; the
  * two differ by at most 1 ulp in log(r2), both within 2 ulp of the reference's normals):
  * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4; 8 = 8-deep load pipeline),
- * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS),
+ * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS: 0 off, 1 element copy,
+ * 2 16-B copy with its loads issued first, the default),
  * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "graph" (steady-state
  * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
 int df_set_tuning(df_handle *h, const char *key, int value);

@@ -261,6 +261,23 @@ def test_table_lds_staging_is_bitexact(spec):
             assert np.array_equal(a.field(k), p.field(k)), k
 
 
+@pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90), (64, 130, 2, 8), (33, 257, 2, 12)])
+def test_table_zstage_copies_are_bitexact(spec):
+    # the three staging copies of the table z-pass (0 none, 1 element copy, 2 16-B copy with loads first):
+    # full and partial groups of 4 strips (6, 9, 2 and 3 strips), odd and even Nz, against packed
+    hs = [gpu_synth(*spec, seed=8, coeff_mode="table") for _ in range(3)]
+    p = gpu_synth(*spec, seed=8, coeff_mode="packed")
+    for level, h in enumerate(hs):
+        h.set_tuning("zstage", level)
+    for _ in range(3):
+        for f in hs + [p]:
+            f.filter(1e-8)
+        for k in FIELDS:
+            for h in hs:
+                assert np.array_equal(h.field(k), p.field(k)), k
+    assert all(h.rng_state() == p.rng_state() for h in hs)
+
+
 @pytest.mark.parametrize("mode", ["packed", "table"])
 def test_graph_path_matches_stream_path(mode):
     # filter() replays a captured HIP graph in the steady state; switching to the stream path

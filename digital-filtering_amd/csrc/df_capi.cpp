@@ -759,7 +759,7 @@ int plan_rng(df_handle *h)
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
     g.gen_compact = 1;
-    g.fast_log = 1; // table-driven log in the polar transform (within 1 ulp of glibc; tests/test_rng_log.py)
+    g.fast_log = 2; // glibc's own log in the polar transform: normals bit-identical (tests/test_rng_log.py)
     if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
     g.nt_stores = 1; // noise written past the caches: it is read once, by the next call's sweeps (A/B -1.4%)
@@ -1648,7 +1648,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
-    else if (k == "fast_log") h->geom.fast_log = value != 0;
+    else if (k == "fast_log") {
+        if (value < 0 || value > 2) return fail(DF_EINVAL, "fast_log must be 0 (device log), 1 (log_r2) or 2 (glibc_log)");
+        h->geom.fast_log = value;
+    }
     else if (k == "graph") h->use_graph = value != 0;
     else if (k == "ywin_T" || k == "zwin_T") {
         if (value < 0 || value > (1 << 24) || (value & (value - 1)))

@@ -335,6 +335,14 @@ template <class G> __device__ bool range_needed(const G &g, uint64_t q0, uint64_
     return false;
 }
 
+// log(r2) of the polar transform (random.tcc:1831): 2 glibc's own log (bit-identical normals, the
+// default), 1 the table-driven log_r2 (within 1 ulp), 0 the device library's log.
+__device__ __forceinline__ double polar_log(const RngGeom &g, double r2)
+{
+    if (g.fast_log == 2) return glibc_log(r2);
+    return g.fast_log ? log_r2(r2, g.log_tab) : log(r2);
+}
+
 // K2c: one thread per wave of attempts (4 per block). A wave's accepted attempts hold ranks
 // [r_lo, r_hi) = block offset + the preceding waves' counts, i.e. stream positions
 // [f + 2 r_lo, f + 2 r_hi). Waves that store something on this GPU (or end the call) are
@@ -485,7 +493,7 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, co
                     } else {
                         a = polar_attempt(s4); // same draws K1 tested
                     }
-                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * (g.fast_log ? log_r2(a.r2, g.log_tab) : log(a.r2)) / a.r2);
+                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * polar_log(g, a.r2) / a.r2);
                     const double xm = a.x * mult;
                     const double ym = a.y * mult;
                     const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;
@@ -618,7 +626,7 @@ __device__ __forceinline__ void gen_batch(const RngGeom &g, const WaveDest &w, c
     } else {
         a = polar_draws(st, s3); // the draws K1 tested; the fourth step only for the call's last attempt
     }
-    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * (g.fast_log ? log_r2(a.r2, g.log_tab) : log(a.r2)) / a.r2);
+    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * polar_log(g, a.r2) / a.r2);
     const double xm = a.x * mult;
     const double ym = a.y * mult;
     const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;

@@ -64,7 +64,8 @@ struct RngGeom {
                                    // iterations, so few-wave planes get short serial chains
     int gen_compact;               // K3 form: 1 = accepted attempts compacted into full batches (default), 0 = sequential
     int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
-    int fast_log;                  // 1: log_r2 (table-driven, df_rng.hpp) in the polar transform; 0: the device library's log
+    int fast_log;                  // log in the polar transform: 2 glibc_log (glibc's bits), 1 log_r2 (table-driven,
+                                   // within 1 ulp), 0 the device library's log (df_rng.hpp)
     const LogTabEntry *log_tab;    // kLogTab entries (build_log_table)
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];

@@ -14,6 +14,8 @@
 #include <cmath>
 #include <cstdint>
 
+#include "glibc_log_table.h"
+
 #ifdef __HIPCC__
 #define DF_HD __host__ __device__ __forceinline__
 #else
@@ -191,6 +193,55 @@ DF_HD double log_r2(double x, const LogTabEntry *tab)
     const double hi = fma(dk, kLn2Hi, e.thi);          // exact
     const double lo = fma(dk, kLn2Lo, e.tlo);
     return hi + (r + (p + lo));
+}
+
+// ---- glibc's own log for r2 in (0, 1] (fast_log 2, the default): the reference's normals come from
+// glibc 2.35's log (random.tcc:1831), which on x86-64 CPUs with FMA is the ifunc __log_fma, i.e.
+// sysdeps/ieee754/dbl-64/e_log.c built with -mfma: r = fma(z, invc, -1) and GCC's contraction of
+// every a*b + c whose product has no other use. Restated here with those fmas explicit, on the
+// constants of glibc_log_table.h; it returns glibc's bits for every argument tested
+// (tests/test_rng_log.py: 1e8 uniform doubles in (0, 1], the near-1 band, powers of two), so the
+// normals, and with them the fields, are bit-identical to the reference's.
+DF_HD double glibc_log(double x)
+{
+    const uint64_t ix = dbits(x);
+    constexpr uint64_t LO = 0x3FEE000000000000ull; // asuint64(1.0 - 0x1p-4)
+    constexpr uint64_t HI = 0x3FF1090000000000ull; // asuint64(1.0 + 0x1.09p-4)
+    if (ix - LO < HI - LO) { // close to 1
+        if (ix == 0x3FF0000000000000ull) return 0.0;
+        const double r = x - 1.0;
+        const double r2 = r * r;
+        const double r3 = r * r2;
+        const double p3 = fma(r3, kGlB[10], fma(r2, kGlB[9], fma(r, kGlB[8], kGlB[7])));
+        const double p2 = fma(r3, p3, fma(r2, kGlB[6], fma(r, kGlB[5], kGlB[4])));
+        const double p1 = fma(r3, p2, fma(r2, kGlB[3], fma(r, kGlB[2], kGlB[1])));
+        double w = r * 0x1p27;
+        const double rhi = r + w - w;
+        const double rlo = r - rhi;
+        w = rhi * rhi * kGlB[0]; // exact (B[0] = -0.5)
+        const double hi = r + w;
+        double lo = r - hi + w;
+        lo = fma(kGlB[0] * rlo, rhi + r, lo);
+        double y = fma(r3, p1, lo); // y = r3 * p1; y += lo
+        y += hi;
+        return y;
+    }
+    constexpr uint64_t OFF = 0x3FE6000000000000ull;
+    const uint64_t tmp = ix - OFF;
+    const int i = (int)((tmp >> 45) & 127);
+    const int k = (int)((int64_t)tmp >> 52);
+    const uint64_t iz = ix - (tmp & (0xFFFull << 52));
+    const double invc = kGlTab[2 * i], logc = kGlTab[2 * i + 1];
+    const double z = dfrom(iz);
+    const double r = fma(z, invc, -1.0);
+    const double kd = (double)k;
+    const double w = fma(kd, kGlLn2Hi, logc);
+    const double hi = w + r;
+    const double lo = fma(kd, kGlLn2Lo, w - hi + r);
+    const double r2 = r * r;
+    const double q = fma(r2, fma(r, kGlA[4], kGlA[3]), fma(r, kGlA[2], kGlA[1]));
+    const double y = fma(r * r2, q, fma(r2, kGlA[0], lo)) + hi;
+    return y;
 }
 
 // The log_r2 table (host): cell centres, 1/c rounded to double, -log(1/c) in x87 long double

@@ -191,8 +191,9 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
                     const long long *dst_cell, long long dst_len, double beta);
 
 /* Launch-shape tuning (extension; results are bit-identical for every setting except "fast_log":
- * 1 (default) = the table-driven log of the polar transform, 0 = the device math library's log; the
- * two differ by at most 1 ulp in log(r2), both within 2 ulp of the reference's normals):
+ * 2 (default) = glibc's own log algorithm in the polar transform (normals and fields bit-identical to
+ * the reference's), 1 = a table-driven log within 1 ulp of it, 0 = the device math library's log;
+ * 1 and 0 keep the normals within 2 ulp of the reference's):
  * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4; 8 = 8-deep load pipeline),
  * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS: 0 off, 1 element copy,
  * 2 16-B copy with its loads issued first, the default),

@@ -101,6 +101,7 @@ struct df_handle {
     // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
+    int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
     // table y-pass: noise and coefficients loaded a whole 4-tap group ahead (ypass_kernel): c3 y-pass
     // 0.141 -> 0.133 ms alone, the reference's grid and c2 -4.5% per call (profiles/r2/ab_ydeep_table.jsonl)
@@ -329,6 +330,9 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
+    // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
+    g.nb_plan = h->rng_blocks;
+    g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
@@ -693,6 +697,10 @@ int plan_strips(df_handle *h)
         // profiles/r2/ab_zsplit.jsonl)
         if (h->coeff_mode == DF_COEFF_PACKED && (long long)h->nstrips * s.Ny < 1024) h->zsplit = 1;
     }
+    // Planes of <= 1024 attempt blocks, table mode: K3 plans its own waves (one launch fewer: the
+    // reference's grid -5% per call, c1/c2 even); packed, its extra waves beside the long y-pass cost
+    // the reference's grid 11% (profiles/r2/ab_fuse_plan.jsonl), so there the scan-and-plan launch stays.
+    h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_ZSPLIT")) h->zsplit = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     const int Ny = s.Ny;
@@ -1658,6 +1666,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
+    else if (k == "fuse_plan") h->fuse_plan = value != 0;
     else if (k == "fast_log") {
         if (value < 0 || value > 2) return fail(DF_EINVAL, "fast_log must be 0 (device log), 1 (log_r2) or 2 (glibc_log)");
         h->geom.fast_log = value;

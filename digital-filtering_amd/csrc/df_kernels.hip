@@ -651,7 +651,10 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
                                                                           RngStateDev *__restrict__ sout,
                                                                           const WaveTask *__restrict__ tasks,
                                                                           const int *__restrict__ ntasks,
-                                                                          const uint16_t *__restrict__ masks)
+                                                                          const uint16_t *__restrict__ masks,
+                                                                          const int *__restrict__ counts_in,
+                                                                          const int *__restrict__ wave_counts_in,
+                                                                          int *__restrict__ err)
 {
     __shared__ uint64_t ring_all[kRngThreads / 64][kGenRing];
     const int lane = threadIdx.x & 63;
@@ -659,14 +662,51 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     const int split = g.gen_split;
     const int vslot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
     const int slot = vslot / split, sub = vslot - slot * split;
-    if (slot >= *ntasks) return;
-    const int gw = uniform(tasks[slot].gw);
-    long long rank_w = tasks[slot].r_lo; // uniform
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    int gw;
+    long long rank_w; // uniform
+    if (g.fused_plan) {
+        // Small planes (g.fused_plan: one GPU, <= 1024 attempt blocks): no scan or plan launch. The wave
+        // is attempt wave `slot`; it sums the accept counts before it (<= 1024 block counts, then its
+        // block's earlier waves) for its first rank, and leaves if it stores nothing here - the same
+        // ranks and the same test as K2 + K2c (rng_scan_plan_small_kernel), so the same bits.
+        constexpr int WPB = kRngThreads / 64;
+        const int nw = g.nb_plan * WPB;
+        if (slot >= nw) return;
+        gw = slot;
+        const int b = gw / WPB, w = gw - b * WPB;
+        long long v = 0;
+        for (int i = lane; i < b; i += 64) v += counts_in[i];
+        if (lane < w) v += wave_counts_in[(size_t)b * WPB + lane];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        rank_w = v;
+        if (vslot == 0) { // once per call: the attempt-shortage check and the cached normal at position 0
+            long long t = 0;
+            for (int i = lane; i < g.nb_plan; i += 64) t += counts_in[i];
+            for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+            if (lane == 0) {
+                if (t < A) *err = 1; // not enough attempts launched (as K2)
+                if (f) {
+                    double *d = stream_dest(g, stream_pos(g, 0));
+                    if (d) *d = sin->saved * 1.0 + 0.0;
+                }
+            }
+        }
+        const long long r_hi = rank_w + wave_counts_in[gw];
+        if (rank_w >= A) return;
+        const uint64_t q_lo = f + 2ull * (uint64_t)rank_w;
+        const uint64_t q_hi = min(f + 2ull * (uint64_t)r_hi, (uint64_t)g.Q);
+        const bool need = (A - 1 < r_hi) || (q_lo < q_hi && range_needed(g, q_lo, q_hi));
+        if (!need) return;
+    } else {
+        if (slot >= *ntasks) return;
+        gw = uniform(tasks[slot].gw);
+        rank_w = tasks[slot].r_lo;
+    }
     const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
     // split counting: only counts were exchanged, so the flags of another rank's blocks are recomputed
     const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const long long A = (long long)((g.Q - f + 1) / 2);
     uint64_t st = thread_first_state(g, sin->state, b, tid);
     const int per = kRngPerThread / split, m0 = sub * per, m1 = m0 + per;
     for (int m = 0; m < m0; ++m) {
@@ -796,7 +836,9 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 #else
     constexpr bool small_ok = true;
 #endif
-    if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {
+    if (g.fused_plan && g.gen_compact) {
+        // the compacted K3 plans its own waves (small planes: one launch fewer per call)
+    } else if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {
         hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
                            wave_counts, nb_scan, nb_total, tasks, ntasks, err);
     } else {
@@ -808,7 +850,7 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
     }
     if (g.gen_compact)
         hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g,
-                           st_in, st_out, tasks, ntasks, masks);
+                           st_in, st_out, tasks, ntasks, masks, counts, wave_counts, err);
     else
         hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in,
                            st_out, tasks, ntasks, masks);

@@ -63,6 +63,8 @@ struct RngGeom {
     int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
                                    // iterations, so few-wave planes get short serial chains
     int gen_compact;               // K3 form: 1 = accepted attempts compacted into full batches (default), 0 = sequential
+    int fused_plan;                // compacted K3 plans its own waves (one GPU, nb_plan <= 1024 blocks): no K2/K2c launch
+    int nb_plan;                   // attempt blocks of the call (fused_plan)
     int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
     int fast_log;                  // log in the polar transform: 2 glibc_log (glibc's bits), 1 log_r2 (table-driven,
                                    // within 1 ulp), 0 the device library's log (df_rng.hpp)

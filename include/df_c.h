@@ -197,7 +197,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * "rows_per_wave" (1,2,4,8), "nt_loads", "heavy_first", "yunroll" (2,4; 8 = 8-deep load pipeline),
  * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS: 0 off, 1 element copy,
  * 2 16-B copy with its loads issued first, the default),
- * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "graph" (steady-state
+ * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "fuse_plan" (planes of
+ * <= 1024 attempt blocks: K3 plans its own waves, one launch fewer; default 1 in table mode), "graph" (steady-state
  * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 

@@ -267,7 +267,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(zsplit=1, nt_loads=0), dict(zsplit=0), dict(ycoop=4), dict(ycoop=4, nt_loads=0),
                 dict(ycoop=7), dict(ycoop=8, nt_loads=0), dict(ycoop=7, ycoop_ovh=64), dict(ycoop_ovh=0),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
-                dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1)]
+                dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
+                dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

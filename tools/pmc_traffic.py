@@ -78,7 +78,7 @@ def main():
             d = os.path.join(a.out, f"{mode}_{counter}")
             run_pmc(counter, d, [sys.executable, os.path.join(ROOT, "bench.py"), "--config", a.config,
                                  "--coeff-mode", mode, "--steps", "3", "--warmup", "1", "--cpu-baseline", "off",
-                                 "--alt-modes", "off"])
+                                 "--alt-modes", "off", "--other-configs", "", "--parity", "off"])
             raw[(mode, counter)] = collapse(parse(d, counter))
     gib = float(1 << 30)
     pf = raw[("probe", "FETCH_SIZE")]

@@ -697,12 +697,14 @@ int plan_strips(df_handle *h)
         // profiles/r2/ab_zsplit.jsonl)
         if (h->coeff_mode == DF_COEFF_PACKED && (long long)h->nstrips * s.Ny < 1024) h->zsplit = 1;
     }
-    // Planes of <= 1024 attempt blocks, table mode: K3 plans its own waves (one launch fewer: the
-    // reference's grid -5% per call, c1/c2 even); packed, its extra waves beside the long y-pass cost
-    // the reference's grid 11% (profiles/r2/ab_fuse_plan.jsonl), so there the scan-and-plan launch stays.
-    h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
+    // Planes of <= 1024 attempt blocks: K3 plans its own waves (one launch fewer: table mode the
+    // reference's grid -5% per call, c1/c2 even; packed c2 -8..-10%, c1 -7%, profiles/r2/
+    // ab_fuse_plan_packed.jsonl). Packed planes with long y chains keep
+    // the scan-and-plan launch: the fused K3's extra waves beside the row-pair y-pass cost the
+    // reference's grid 11% (profiles/r2/ab_fuse_plan.jsonl).
     if (const char *e = std::getenv("DFAMD_ZSPLIT")) h->zsplit = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
+    h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE || h->ycoop < 7 ? 1 : 0;
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];

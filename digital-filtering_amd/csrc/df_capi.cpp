@@ -987,19 +987,7 @@ int alloc_components(df_handle *h)
             total += ((size_t)(dir ? d.bz_elems : d.by_elems) + align - 1) / align * align;
         }
         double *base = nullptr;
-        // The pool is asked for physically contiguous memory (hipDeviceMallocContiguous), falling back to
-        // a plain allocation when the driver cannot provide it: c3 3.35 -> 3.30 and 3.39 -> 3.30 ms per
-        // call (mean of 8 handles on each of two boxes, and a narrower spread; profiles/r2/contig/).
-        // DFAMD_B_CONTIG=0 skips the request.
-        const char *ce = std::getenv("DFAMD_B_CONTIG");
-        if ((!ce || std::atoi(ce)) &&
-            hipExtMallocWithFlags((void **)&base, total * sizeof(double), hipDeviceMallocContiguous) == hipSuccess) {
-            h->allocs.push_back(base);
-            HIP_OR(hipMemsetAsync(base, 0, total * sizeof(double), h->stream), DF_EHIP);
-        } else {
-            (void)hipGetLastError();
-            if ((rc = dalloc_t(h, &base, total))) return rc;
-        }
+        if ((rc = dalloc_t(h, &base, total))) return rc;
         for (int k = 0; k < 6; ++k) {
             CompDev &d = h->c[pool == 1 ? k >> 1 : k % 3];
             const int dir = pool == 1 ? k & 1 : k / 3;

@@ -905,8 +905,9 @@ int alloc_components(df_handle *h)
     // Packed mode: the six coefficient arrays (By0 Bz0 By1 Bz1 By2 Bz2, each 2 MiB aligned) share ONE
     // allocation instead of one each: c3 3.47-3.51 -> 3.37-3.41 ms per call, mean over 8 handles on each
     // of two boxes (profiles/r2/pool/; order By0 By1 By2 Bz0 Bz1 Bz2 = 2 gains a little less). Same
-    // bytes, same kernels: where the 20 GB stream lands is all that changes (a single large allocation
-    // is placed in larger physical fragments). DFAMD_B_POOL=0 allocates them one by one.
+    // bytes, same kernels: where the 20 GB stream lands is all that changes (presumably larger physical
+    // fragments for one large allocation, i.e. fewer address-translation misses; not measured).
+    // DFAMD_B_POOL=0 allocates them one by one.
     int pool = 1;
     if (const char *e = std::getenv("DFAMD_B_POOL")) pool = std::atoi(e);
     const int Ny = s.Ny;

@@ -18,10 +18,18 @@ plane unsplit in table mode on its own GPU and compares its strip bit for bit (p
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--coeff-mode packed|table]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` with N > 1 outside a torchrun launch starts one itself: before torch is
+imported or any GPU touched, it runs `python -m torch.distributed.run --nproc-per-node N bench.py
+...` as a CHILD process (never exec), relays rank 0's JSON line to stdout and exits with the
+child's return code. At N > 1 rank 0 also times the whole plane unsplit on its own GPU after the
+timed region (`same_plane_1gpu`: the 1-GPU time of the SAME plane, and the speedup over it), and
+the c5 line runs BASELINE configs[4]'s 10 000 filter(dt) steps for real (`long_run`).
 """
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import time
@@ -90,8 +98,59 @@ def parse(argv=None):
                         "auto: 'native,c2' on one GPU, 'c5' on N > 1; '' for none")
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
                    help="also time the other coefficient mode (N=1 only) and report it under alt_modes")
+    p.add_argument("--same-plane", default="auto", choices=["auto", "off"],
+                   help="N > 1: rank 0 also times the whole plane unsplit on its own GPU (same_plane_1gpu)")
+    p.add_argument("--long-run", default="auto",
+                   help="filter(dt) calls of the long run (device get_rms accumulation every call, steady-state "
+                        "and total time, the SURVEY 4 variance invariant at the end); auto: 10000 on c5 at N > 1 "
+                        "(BASELINE configs[4]), else none; an integer K runs K calls on the main workload")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launch plumbing only: every rank reports its env, rank 0 prints one JSON line; no GPU")
+    p.add_argument("--dropin", default="auto", choices=["auto", "off"],
+                   help="N=1: time the C++ drop-in (examples/cpp-test) DIGITAL_FILTER::filter() wall per call")
     a = p.parse_args(argv)
     return a
+
+
+def progress(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_command(argv, n, port):
+    """The torchrun command a bare `bench.py --gpus N` (N > 1) starts as its child: one rank per GPU
+    of this node, rendezvous on 127.0.0.1, the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def self_launch(argv, n, cmd=None):
+    """Run the N-rank bench as a child process (never os.exec*: this process has not touched the GPU
+    and must not replace itself), relay its JSON line (the one rank 0 prints) to stdout and everything
+    else to stderr, and return the child's return code (1 if it succeeded without a JSON line)."""
+    cmd = cmd or launch_command(argv, n, free_port())
+    progress("launching " + " ".join(cmd))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line_out = None
+    for line in proc.stdout:
+        st = line.strip()
+        if st.startswith("{") and '"metric"' in st:
+            line_out = st
+            print(st, flush=True)
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if rc == 0 and line_out is None:
+        progress("the launched ranks exited 0 without a JSON line")
+        rc = 1
+    return rc
 
 
 def host_cpu():
@@ -182,6 +241,33 @@ def cpu_baseline_parallel(args, Ny, N_min, N_max):
                     "(RNG serial); not the reference, which is single-threaded"}
 
 
+def dropin_timing(args):
+    """The C++ drop-in's per-call cost: examples/cpp-test `time` runs, on one object,
+    the C-ABI call (df_filter + df_sync) and DIGITAL_FILTER::filter() with host_mirror 0 (no host
+    copies), 1 (default: u/v/w.fluc, T', rho' - one sync, page-locked vectors) and 2 (also filt_old and
+    filt), on the reference's grid and on c3, in both coefficient modes. The mirror refresh is a PCIe
+    D2H transfer of 5 (or 8) fields; `mirror1_GBps` is its rate."""
+    exe = os.path.join(ROOT, "examples", "cpp-test")
+    if not os.path.exists(exe):
+        return {"error": "examples/cpp-test not built (make -C examples)"}
+    out = {}
+    for plane, dims in (("native", ("0", "0", "0", "0")), ("c3", ("2048", "2048", "4", "64"))):
+        for mode in ("table", "packed"):
+            progress(f"drop-in timing {plane} {mode}")
+            try:
+                r = subprocess.run([exe, "time", "native" if plane == "native" else "synth", *dims, mode, "20"],
+                                   capture_output=True, text=True, timeout=300, check=True)
+                rec = json.loads(r.stdout.strip().splitlines()[-1])
+                d = rec["dropin_ms"]
+                extra = d["mirror1"] - d["mirror0"]
+                rec["mirror1_GBps"] = round(rec["mirror_bytes"]["mirror1"] / (extra * 1e-3) / 1e9, 1) if extra > 0 else None
+                rec["dropin_over_capi"] = round(d["mirror1"] / rec["capi_ms"], 3)
+                out[f"{plane}/{mode}"] = rec
+            except Exception as e:  # reported, never fatal for the GPU number
+                out[f"{plane}/{mode}"] = {"error": str(e)[-400:]}
+    return out
+
+
 class Ctx:
     """Process-group plumbing: rank, world, device and the gather/reduce helpers."""
 
@@ -243,7 +329,7 @@ def make_filter(dfamd, ctx, wl, args, coeff_mode, split=True, comm_id=None):
     return dfamd.DigitalFilter(**kw)
 
 
-def timed(ctx, h, args, min_warm_s=0.0, profile=True):
+def timed(ctx, h, args, min_warm_s=0.0, profile=True, collective=True):
     """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile.
     min_warm_s > 0 (secondary lines only: alt mode, other configs) keeps warming up until that much
     time has passed: a 0.4 ms table-mode call otherwise starts timing while the clocks still ramp
@@ -256,20 +342,22 @@ def timed(ctx, h, args, min_warm_s=0.0, profile=True):
     h.sync()
     t_w = time.perf_counter()
     # one process only: every call of a split plane is an RCCL exchange, so ranks must run equal counts
-    while min_warm_s > 0 and ctx.world == 1 and time.perf_counter() - t_w < min_warm_s:
+    while min_warm_s > 0 and (ctx.world == 1 or not collective) and time.perf_counter() - t_w < min_warm_s:
         for _ in range(10):
             h.filter(args.dt)
             calls += 1
         h.sync()
     h.set_profiling(profile)
-    ctx.barrier()
+    if collective:
+        ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         h.filter(args.dt)
     h.sync()
     torch.cuda.synchronize()
-    ctx.barrier()
+    if collective:
+        ctx.barrier()
     el = time.perf_counter() - t0
     prof = h.profile() if profile else None
     h.set_profiling(False)
@@ -355,6 +443,85 @@ def run_config(dfamd, ctx, wl, args, comm_id, min_warm_s=0.0):
     return f, rank_rec
 
 
+def same_plane_1gpu(dfamd, ctx, wl, args, split_ms):
+    """N > 1, rank 0: the whole plane unsplit on its own GPU, same mode, K and W, after every rank has
+    closed its strip: the 1-GPU time of the SAME plane the N ranks split, and the speedup over it.
+    The other ranks wait at the barrier. (near-linear vs 1 GPU on one plane.)"""
+    res = None
+    if ctx.rank == 0:
+        progress(f"{wl['name']}: whole plane on one GPU (same-plane baseline)")
+        h = make_filter(dfamd, ctx, wl, args, args.coeff_mode, split=False)
+        el, prof, _ = timed(ctx, h, args, collective=False)
+        roof = roofline_of(h, prof, args, wl["name"])
+        h.close()
+        ms = el * 1e3 / args.steps
+        res = {"ms_per_step": round(ms, 4), "value": round(wl["Ny"] * wl["Nz"] * args.steps / el, 1),
+               "phase_ms_per_call": per_call(prof), "roofline_frac": roof["frac"],
+               "speedup": round(ms / split_ms, 3),
+               "note": "rank 0 alone, whole plane unsplit on its GPU after the timed region; speedup = this "
+                       "ms_per_step / the N-rank ms_per_step (max over ranks)"}
+    ctx.barrier()
+    return res
+
+
+def long_run(dfamd, ctx, wl, args, steps, comm_id):
+    """BASELINE configs[4]'s run for real: `steps` filter(dt) calls, each followed by the device
+    get_rms accumulation (df.cpp:584-611: filter, then rms_add), timed as a whole (barrier +
+    synchronize on both sides, max over ranks) and in windows of steps/10 calls (steady state). At the
+    end, SURVEY 4's invariant over the whole plane: per row, the mean of u'^2, v'^2, w'^2 over time
+    and every rank's columns against R11, R22, R33 (rows with R11 > 1% of its max)."""
+    torch = ctx.torch
+    h = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
+    h.filter(args.dt)
+    h.sync()
+    h.rms_reset()
+    win = max(1, steps // 10)
+    windows = []
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = last = time.perf_counter()
+    for i in range(steps):
+        h.filter(args.dt)
+        h.rms_add()
+        if (i + 1) % win == 0 or i + 1 == steps:
+            h.sync()
+            now = time.perf_counter()
+            n = (i + 1) - (len(windows) * win)
+            windows.append(round((now - last) * 1e3 / n, 4))
+            last = now
+            if ctx.rank == 0:
+                progress(f"long run {wl['name']}: {i + 1}/{steps} calls, {windows[-1]} ms/call")
+    h.sync()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    total = time.perf_counter() - t0
+    sums = {k: (h.rms(k) ** 2).sum(axis=1) for k in ("u", "v", "w")}  # per row, this strip's columns
+    rows = {k: h.row(k) for k in ("R11", "R22", "R33")}
+    finite = bool(all(np.isfinite(h.field(k)).all() for k in FIELDS))
+    state = h.rng_state()
+    h.close()
+    recs = ctx.gather({"total_s": total, "windows": windows, "sums": sums, "finite": finite,
+                       "rng_state": [str(state[0]), int(state[1])]})
+    if ctx.rank != 0:
+        return None
+    R = rows
+    mask = R["R11"] > 0.01 * R["R11"].max()
+    dev = {}
+    for name, r in (("u", "R11"), ("v", "R22"), ("w", "R33")):
+        ms2 = sum(x["sums"][name] for x in recs) / wl["Nz"]
+        dev[name] = round(float(np.abs(ms2[mask] / R[r][mask] - 1).max()), 4)
+    tot = max(x["total_s"] for x in recs)
+    steady = [max(x["windows"][i] for x in recs) for i in range(len(recs[0]["windows"]))]
+    return {"steps": steps, "total_s": round(tot, 3), "ms_per_call_incl_rms": round(tot * 1e3 / steps, 4),
+            "steady_ms_per_call": round(float(np.median(steady[1:] if len(steady) > 1 else steady)), 4),
+            "window_ms_per_call": steady, "window_calls": win,
+            "max_rel_dev_rowvar_vs_R": dev, "rows_checked": int(mask.sum()),
+            "fields_finite": all(x["finite"] for x in recs),
+            "rng_state_equal_on_ranks": len({tuple(x["rng_state"]) for x in recs}) == 1,
+            "note": "every call = filter(dt) + rms_add on the device (the reference's get_rms loop, "
+                    "df.cpp:596-606); times max over ranks; windows of window_calls calls"}
+
+
 def summarize(ctx, wl, args, recs):
     """Whole-job numbers from every rank's record (max-over-ranks time)."""
     el_max = max(r["elapsed_s"] for r in recs)
@@ -385,11 +552,18 @@ def summarize(ctx, wl, args, recs):
 
 
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     args = parse(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # a bare `bench.py --gpus N`: start the N ranks as a child torchrun (torch not imported yet)
+        return self_launch(argv, args.gpus)
     ctx = Ctx()
+    if args.dry_run:  # tests/test_bench_launch.py: the self-launch reaches N ranks with the right env
+        if ctx.rank == 0:
+            print(json.dumps({"metric": "dry-run", "n_gpus": ctx.world, "gpus_arg": args.gpus,
+                              "master_addr": os.environ.get("MASTER_ADDR"), "argv": argv}), flush=True)
+        return 0
     if ctx.world != args.gpus:
-        if ctx.world == 1 and args.gpus > 1:
-            sys.exit("for --gpus > 1 launch with torch.distributed.run --nproc-per-node N")
         args.gpus = ctx.world
     name = args.config if args.config != "auto" else ("c3" if ctx.world == 1 else "c4")
     wl = plan_workload(name, ctx.world, args.scaling)
@@ -404,6 +578,8 @@ def main(argv=None):
     import dfamd
 
     comm_id = ctx.comm_id(dfamd)
+    if ctx.rank == 0:
+        progress(f"{name}: {wl['Ny']}x{wl['Nz']} over {ctx.world} rank(s), {args.coeff_mode}")
     f, rec = run_config(dfamd, ctx, wl, args, comm_id)
     recs = ctx.gather(rec)
     head = summarize(ctx, wl, args, recs)
@@ -451,6 +627,12 @@ def main(argv=None):
                   "calls_compared": f.calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
     comm = f.comm_info() if ctx.world > 1 else None
     f.close()
+    ctx.barrier()
+    same = None
+    if ctx.world > 1 and args.same_plane == "auto":
+        same = same_plane_1gpu(dfamd, ctx, wl, args, head["ms_per_step"])
+    lr_steps = 0 if args.long_run == "auto" else int(args.long_run)
+    lr = long_run(dfamd, ctx, wl, args, lr_steps, ctx.comm_id(dfamd)) if lr_steps > 0 else None
 
     others = {}
     for oname in filter(None, others_arg.split(",")):
@@ -460,6 +642,8 @@ def main(argv=None):
             owl = plan_workload(oname, ctx.world, args.scaling)
         except ValueError:
             continue
+        if ctx.rank == 0:
+            progress(f"{oname}: {owl['Ny']}x{owl['Nz']} over {ctx.world} rank(s)")
         h, orec = run_config(dfamd, ctx, owl, args, ctx.comm_id(dfamd), min_warm_s=0.3)
         orecs = ctx.gather(orec)
         osum = summarize(ctx, owl, args, orecs)
@@ -468,13 +652,19 @@ def main(argv=None):
             ops = ctx.gather(parity_check(dfamd, ctx, owl, args, h, h.calls_done))
             op = all(p["ok"] for p in ops)
         h.close()
+        ctx.barrier()
         others[oname] = {"workload": owl["desc"], "Ny": owl["Ny"], "Nz": owl["Nz"], "scaling": owl["scaling"],
                          "parity_ok": op, **osum}
         if ops and not op:
             others[oname]["parity"] = [p for p in ops if not p["ok"]]
-        if oname == "c5":
-            others[oname]["projected_10k_steps_s"] = round(osum["ms_per_step"] * 10.0, 2)
+        if ctx.world > 1 and args.same_plane == "auto":
+            others[oname]["same_plane_1gpu"] = same_plane_1gpu(dfamd, ctx, owl, args, osum["ms_per_step"])
+        if oname == "c5" and ctx.world > 1 and args.long_run == "auto":
+            others[oname]["long_run"] = long_run(dfamd, ctx, owl, args, 10000, ctx.comm_id(dfamd))
 
+    dropin = None
+    if ctx.rank == 0 and ctx.world == 1 and args.dropin == "auto":
+        dropin = dropin_timing(args)
     if ctx.rank == 0:
         cpu = cpu_par = None
         if args.cpu_baseline == "auto" and ctx.world == 1 and wl["plane"] != "native":
@@ -521,6 +711,14 @@ def main(argv=None):
         out["call_hbm_frac"] = round(call_bytes / (ms * 1e-3) / 1e9 / (HBM_PEAK_GBPS * ctx.world), 4)
         if "multi_gpu" in head:
             out["multi_gpu"] = head["multi_gpu"]
+        if same is not None:
+            out["ms_per_step_1gpu_same_plane"] = same["ms_per_step"]
+            out["speedup"] = same["speedup"]
+            out["same_plane_1gpu"] = same
+        if lr is not None:
+            out["long_run"] = lr
+        if dropin is not None:
+            out["dropin"] = dropin
         print(json.dumps(out), flush=True)
     ctx.barrier()
     if ctx.dist is not None:

@@ -23,7 +23,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -168,6 +170,51 @@ struct df_handle {
 
 namespace {
 
+// Process-wide registry of every live device range the library allocated, all handles together.
+// A new allocation that overlaps a live one fails loudly instead of aliasing another handle's buffer
+// (round 2 saw one handle's T' change after a second handle was created while the coefficient pool
+// was requested physically contiguous; the cause was not pinned down - DESIGN.md section 3).
+struct AllocRegistry {
+    std::mutex mu;
+    std::map<uintptr_t, std::pair<uintptr_t, const void *>> live; // start -> (end, owner)
+};
+AllocRegistry &registry()
+{
+    static AllocRegistry r;
+    return r;
+}
+std::string hex_range(uintptr_t a, uintptr_t b)
+{
+    char buf[64];
+    std::snprintf(buf, sizeof buf, "[0x%llx, 0x%llx)", (unsigned long long)a, (unsigned long long)b);
+    return buf;
+}
+// Claim [p, p + bytes) for owner; DF_EHIP naming both ranges if it overlaps a live range.
+int registry_claim(const void *p, size_t bytes, const void *owner)
+{
+    const uintptr_t a = (uintptr_t)p, b = a + bytes;
+    AllocRegistry &r = registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    auto it = r.live.upper_bound(a); // first start > a; its predecessor may still cover a
+    if (it != r.live.begin()) {
+        auto prev = std::prev(it);
+        if (prev->second.first > a)
+            return fail(DF_EHIP, "device allocation " + hex_range(a, b) + " overlaps the live range " +
+                                     hex_range(prev->first, prev->second.first) + (prev->second.second == owner ? " of the same handle" : " of another handle"));
+    }
+    if (it != r.live.end() && it->first < b)
+        return fail(DF_EHIP, "device allocation " + hex_range(a, b) + " overlaps the live range " +
+                                 hex_range(it->first, it->second.first) + (it->second.second == owner ? " of the same handle" : " of another handle"));
+    r.live.emplace(a, std::make_pair(b, owner));
+    return DF_OK;
+}
+void registry_release(const void *p)
+{
+    AllocRegistry &r = registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    r.live.erase((uintptr_t)p);
+}
+
 int dalloc(df_handle *h, void **p, size_t bytes)
 {
     if (bytes == 0) bytes = 16;
@@ -177,6 +224,11 @@ int dalloc(df_handle *h, void **p, size_t bytes)
                                  // (hipGetLastError after a kernel) would report it as its own
         return fail(e == hipErrorOutOfMemory ? DF_ENOMEM : DF_EHIP,
                     "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    }
+    if (int rc = registry_claim(*p, bytes, h)) {
+        (void)hipFree(*p);
+        *p = nullptr;
+        return rc;
     }
     h->allocs.push_back(*p);
     HIP_OR(hipMemsetAsync(*p, 0, bytes, h->stream), DF_EHIP);
@@ -635,6 +687,8 @@ void balance_ycoop2(df_handle *h, int c)
     constexpr int RR = 2; // rows per block of the row-pair y-pass
     const int Ny = h->Ny, nrb = (Ny + RR - 1) / RR;
     const std::vector<int> &Nst = h->y_nst[c];
+    // host-only handles (no device state) never built the tap ranges: nothing to balance
+    if (Nst.size() < (size_t)h->nstrips * Ny) return;
     std::vector<double> wgt((size_t)h->nstrips * nrb);
     const double ovh = (double)h->ycoop_ovh * kStrip;
     double tot = 0;
@@ -1127,7 +1181,10 @@ void destroy(df_handle *h)
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
-    for (void *p : h->allocs) (void)hipFree(p);
+    for (void *p : h->allocs) {
+        (void)hipFree(p);
+        registry_release(p);
+    }
     if (h->err_host) (void)hipHostFree(h->err_host);
     if (h->rng_comm) ncclCommDestroy(h->rng_comm);
     if (h->comm) ncclCommDestroy(h->comm);
@@ -1488,6 +1545,52 @@ int df_get_field(df_handle *h, int which, double *out)
     HIP_OR(hipMemcpyAsync(out, src, (size_t)h->Ny * h->Nz_loc * 8, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     return check_rng_error(h);
+}
+
+int df_get_fields(df_handle *h, int n, const int *which, double *const *host_out)
+{
+    // The C++ mirrors' per-call refresh: every copy queued on the handle's stream, ONE synchronisation.
+    // Into pinned memory (df_host_pin) the copies are DMA transfers that overlap each other's setup;
+    // into pageable memory the runtime stages them (still one host wait at the end).
+    if (!valid_out(h) || n < 0 || (n && (!which || !host_out))) return fail(DF_EINVAL, "df_get_fields: bad arguments");
+    const size_t bytes = (size_t)h->Ny * h->Nz_loc * 8;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    for (int i = 0; i < n; ++i) {
+        const double *src = df_device_field(h, which[i]);
+        if (!src || !host_out[i]) return fail(DF_EINVAL, "df_get_fields: field " + std::to_string(i));
+        HIP_OR(hipMemcpyAsync(host_out[i], src, bytes, hipMemcpyDeviceToHost, h->stream), DF_EHIP);
+    }
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return check_rng_error(h);
+}
+
+int df_alloc_registry(const void *p, size_t bytes, int claim)
+{
+    if (!p || (claim && !bytes)) return fail(DF_EINVAL, "df_alloc_registry: null or empty range");
+    if (claim) return registry_claim(p, bytes, nullptr);
+    registry_release(p);
+    return DF_OK;
+}
+
+long long df_alloc_registry_count(void)
+{
+    AllocRegistry &r = registry();
+    std::lock_guard<std::mutex> lk(r.mu);
+    return (long long)r.live.size();
+}
+
+int df_host_pin(void *p, size_t bytes)
+{
+    if (!p || !bytes) return fail(DF_EINVAL, "df_host_pin: null or empty range");
+    HIP_OR(hipHostRegister(p, bytes, hipHostRegisterDefault), DF_EHIP);
+    return DF_OK;
+}
+
+int df_host_unpin(void *p)
+{
+    if (!p) return fail(DF_EINVAL, "df_host_unpin: null pointer");
+    HIP_OR(hipHostUnregister(p), DF_EHIP);
+    return DF_OK;
 }
 
 int df_set_field(df_handle *h, int which, const double *host_in)

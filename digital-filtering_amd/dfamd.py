@@ -150,7 +150,15 @@ def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_m
                 rank=0, world=1, comm_id=None, csv_path=None, rows_per_wave=0, rst_file=None, line_file=None,
                 d_i=None, rho_e=None, U_e=None, mu_e=None, resume=None, grid_y=None, grid_z=None, grid_file=None):
     """resume = (pcg state, saved_flag, saved): start the stream there instead of seeding.
-    plane="grid": grid_y / grid_z vertex arrays of shape (Ny+1, Nz+1) (Ny, Nz cells), or grid_file."""
+    plane="grid": grid_y / grid_z vertex arrays of shape (Ny+1, Nz+1) (Ny, Nz cells), or grid_file.
+
+    coeff_mode defaults to "packed" here, NOT to df_config_default's DF_COEFF_TABLE: this mirror
+    serves the tests and bench.py, which exercise the reference's offset-packed data contract (the
+    HBM roofline point). The fields are bit-identical either way, but the launch plan follows the
+    mode: packed replicates the RNG counting (halo = the only collective), allocates the 20-85 GB
+    coefficient stream and uses the row-pair y-pass on long chains; table splits the counting (one
+    all-gather of counts per call) and allocates no stream. Pass coeff_mode="table" to get the
+    C/C++/Fortran drop-in default."""
     cfg = _Cfg()
     lib().df_config_default(C.byref(cfg))
     keep = []

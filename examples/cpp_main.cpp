@@ -10,12 +10,63 @@
 //                                 plot_RST_lerp() -> ../files/myRST.csv, ../files/duanRST.csv
 //   cpp-test twin Ny Nz Nmin Nmax seed steps csvA csvB   two objects on the process's one stream
 //                                 (df.cpp:334-335): A then B constructed, filter calls alternating
+//   cpp-test time native|synth Ny Nz Nmin Nmax packed|table calls   one JSON line: wall ms per call
+//                                 of the C-ABI call (df_filter + df_sync) and of DIGITAL_FILTER::filter()
+//                                 with host_mirror 0, 1, 2 on the same object (bench.py `dropin`)
 #include "df.hpp"
 
 #include <cstdlib>
 
+static int time_dropin(char **argv)
+{
+    DFConfig config;
+    config.plane = std::string(argv[2]) == "native" ? DF_PLANE_NATIVE : DF_PLANE_SYNTHETIC;
+    config.Ny = std::atoi(argv[3]);
+    config.Nz = std::atoi(argv[4]);
+    config.N_min = std::atoi(argv[5]);
+    config.N_max = std::atoi(argv[6]);
+    config.coeff_mode = std::string(argv[7]) == "packed" ? DF_COEFF_PACKED : DF_COEFF_TABLE;
+    const int calls = std::atoi(argv[8]);
+    config.seed = 42;
+    config.seed_from_random_device = false;
+    config.verbose = false;
+    config.mirror_coefficients = 0;
+    DIGITAL_FILTER df(config);
+    df_handle *h = df.handle();
+    int ny, nz, z0, z1;
+    df_dims(h, &ny, &nz, &z0, &z1);
+    const double cells = (double)ny * (z1 - z0);
+    auto wall = [&](auto &&call) {
+        for (int i = 0; i < 5; ++i) call();
+        auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; i < calls; ++i) call();
+        auto t1 = std::chrono::steady_clock::now();
+        return std::chrono::duration<double, std::milli>(t1 - t0).count() / calls;
+    };
+    auto ok = [](int rc) {
+        if (rc != DF_OK) throw std::runtime_error(df_last_error());
+    };
+    const double capi_async = wall([&] { ok(df_filter(h, 1e-8)); }) ; // queue only; the sync below drains
+    ok(df_sync(h));
+    const double capi = wall([&] { ok(df_filter(h, 1e-8)); ok(df_sync(h)); });
+    double dropin[3];
+    for (int m = 0; m < 3; ++m) {
+        df.set_host_mirror(m);
+        dropin[m] = wall([&] { df.filter(1e-8); });
+    }
+    std::cout << std::setprecision(6) << "{\"plane\": \"" << argv[2] << "\", \"Ny\": " << ny << ", \"Nz\": " << nz
+              << ", \"coeff_mode\": \"" << argv[7] << "\", \"calls\": " << calls
+              << ", \"capi_ms\": " << capi << ", \"capi_async_ms\": " << capi_async
+              << ", \"dropin_ms\": {\"mirror0\": " << dropin[0] << ", \"mirror1\": " << dropin[1]
+              << ", \"mirror2\": " << dropin[2] << "}, \"mirror_bytes\": {\"mirror1\": " << 5 * 8 * cells
+              << ", \"mirror2\": " << 8 * 8 * cells << "}}" << std::endl;
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc >= 9 && std::string(argv[1]) == "time") return time_dropin(argv);
+
     // Create configuration struct
     DFConfig config;
     if (argc > 1 && std::string(argv[1]) == "synth" && argc >= 8) {

@@ -8,7 +8,9 @@
 // Everything runs on the GPU through the C ABI in df_c.h (libdfamd.so); the
 // public FilterField vectors are host mirrors refreshed after each call
 // (DFConfig::host_mirror), the device copies are reachable zero-copy through
-// device_field().
+// device_field(). Default (host_mirror 1): u/v/w.fluc, T', rho' after every call with
+// one synchronisation into page-locked vectors; filt_old/filt on request (sync_host(), checkpoint())
+// or every call with host_mirror 2.
 //
 // Deliberate differences: DFConfig fields are honoured
 // (the reference ignores them; their defaults here are its hard-coded values);
@@ -71,14 +73,29 @@ struct DFCheckpoint {
 // statics of generate_white_noise (df.cpp:334-335): the first object to draw seeds it, later objects
 // continue it in call order (constructor step 0 included). Each handle here owns a device-side copy
 // of the stream; with DFConfig::shared_stream the objects of a process hand this one state on: an
-// object that draws after another first loads the shared state into its handle (df_set_rng_state,
-// which regenerates the prefetched noise), and every draw publishes the state it leaves.
+// object that draws after another first loads the shared state into its handle (df_set_rng_state).
+// The state is read back from the device only when another object needs it (or the holder is
+// destroyed), so a single object's filter() pays no per-call state copy.
+// Cost and ordering: every switch between objects synchronizes both handles and regenerates the
+// prefetched noise of the one that draws next (one noise generation, plus, on an RCCL handle with
+// split counting - the table-mode default - its counts all-gather). Multi-rank programs must
+// therefore construct their objects and call them in the same order on every rank.
 struct DFSharedStream {
     bool seeded = false;
+    bool stale = false;          // state/saved are older than the holder's device copy
     std::uint64_t state = 0;
     int saved_flag = 0;
     double saved = 0.0;
-    const void *last = nullptr; // the object whose handle holds the current state
+    const void *last = nullptr;  // the object whose handle holds the current state
+    df_handle *last_h = nullptr; // its handle (read back from it when stale)
+    void materialize()
+    {
+        if (stale && last_h) {
+            if (df_rng_state(last_h, &state, &saved_flag, &saved) != DF_OK)
+                throw std::runtime_error(std::string("libdfamd: ") + df_last_error());
+            stale = false;
+        }
+    }
 };
 inline DFSharedStream &df_shared_stream()
 {
@@ -106,10 +123,16 @@ struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     int device = 0;
     int rank = 0, world = 1;
     const void *comm_id = nullptr;
-    int host_mirror = 1;         // 1: refresh u/v/w.fluc, filt_old, T', rho' after every call; 0: never
+    // Host mirrors (the reference's public vectors, df.hpp:28, 59): 1 (default) refreshes u/v/w.fluc,
+    // T', rho' after every call - one stream synchronisation, DMA into page-locked vectors; filt_old
+    // and filt are refreshed on request (sync_host(), checkpoint()). 2: all of them after every call.
+    // 0: never (a GPU-resident solver reads device_field()).
+    int host_mirror = 1;
+    bool pin_mirrors = true;     // page-lock the mirror vectors (hipHostRegister via df_host_pin)
     int mirror_coefficients = -1; // by/bz host copies: 1 always, 0 never, -1 when <= 1 GiB
     bool verbose = true;         // print "Filtering took X seconds." (df.cpp:464)
     bool shared_stream = true;   // one stream for every object of the process, as the reference's statics
+                                 // (see DFSharedStream: per-switch cost; same object order on every rank)
     bool resume = false;         // start the stream at (rng_state, rng_saved_flag, rng_saved)
     std::uint64_t rng_state = 0;
     int rng_saved_flag = 0;
@@ -152,21 +175,55 @@ class DIGITAL_FILTER {
         dst.resize(n_cells);
         check(df_get_field(h_, which, dst.data()));
     }
-    void refresh()
+    // Page-locked mirrors: each registered range, re-registered when a vector's buffer moved.
+    struct Pin {
+        const void *p = nullptr;
+        size_t bytes = 0;
+        const void *refused = nullptr; // the runtime refused this buffer: do not retry every call
+    };
+    Pin pins_[8];
+    void pin(Vector &v, Pin &pn)
     {
-        if (!cfg_.host_mirror) return;
-        pull(u.fluc, DF_U);
-        pull(v.fluc, DF_V);
-        pull(w.fluc, DF_W);
-        pull(u.filt_old, DF_FILT_OLD_U);
-        pull(v.filt_old, DF_FILT_OLD_V);
-        pull(w.filt_old, DF_FILT_OLD_W);
-        pull(T_fluc, DF_T);
-        pull(rho_fluc, DF_RHO);
-        // after apply_RST_scaling the reference's filt equals filt_old (df.cpp:440-442)
-        u.filt = u.filt_old;
-        v.filt = v.filt_old;
-        w.filt = w.filt_old;
+        v.resize(n_cells);
+        const size_t bytes = v.size() * sizeof(double);
+        if (!cfg_.pin_mirrors || bytes == 0 || (pn.p == v.data() && pn.bytes == bytes) || pn.refused == v.data())
+            return;
+        if (pn.p) df_host_unpin(const_cast<void *>(pn.p));
+        pn = Pin{};
+        if (df_host_pin(v.data(), bytes) == DF_OK) pn = Pin{v.data(), bytes, nullptr};
+        else pn.refused = v.data(); // pageable copies still work, at the runtime's staging rate
+    }
+    void unpin_all()
+    {
+        for (Pin &pn : pins_)
+            if (pn.p) df_host_unpin(const_cast<void *>(pn.p));
+        for (Pin &pn : pins_) pn = Pin{};
+    }
+    // Every mirror in one df_get_fields: one stream synchronisation per refresh.
+    void refresh_mirrors(bool with_filt_old)
+    {
+        Vector *dst[8] = {&u.fluc, &v.fluc, &w.fluc, &T_fluc, &rho_fluc, &u.filt_old, &v.filt_old, &w.filt_old};
+        const int which[8] = {DF_U, DF_V, DF_W, DF_T, DF_RHO, DF_FILT_OLD_U, DF_FILT_OLD_V, DF_FILT_OLD_W};
+        const int n = with_filt_old ? 8 : 5;
+        double *out[8];
+        for (int i = 0; i < n; ++i) {
+            pin(*dst[i], pins_[i]);
+            out[i] = dst[i]->data();
+        }
+        check(df_get_fields(h_, n, which, out));
+        if (with_filt_old) { // after apply_RST_scaling the reference's filt equals filt_old (df.cpp:440-442)
+            u.filt = u.filt_old;
+            v.filt = v.filt_old;
+            w.filt = w.filt_old;
+        }
+    }
+    void refresh() // after filter() / get_rms(): the per-call set
+    {
+        if (cfg_.host_mirror) refresh_mirrors(cfg_.host_mirror >= 2);
+    }
+    void refresh_full() // construction, stage API, restore: every mirror (not per call)
+    {
+        if (cfg_.host_mirror) refresh_mirrors(true);
     }
     void fill_field(FilterField &F, int c)
     {
@@ -227,6 +284,7 @@ class DIGITAL_FILTER {
         c.rng_saved = config.rng_saved;
         DFSharedStream &ss = df_shared_stream();
         if (config.shared_stream && !config.resume && ss.seeded) { // step 0 continues the process's stream
+            ss.materialize();
             c.rng_resume = 1;
             c.rng_state = ss.state;
             c.rng_saved_flag = ss.saved_flag;
@@ -248,7 +306,15 @@ class DIGITAL_FILTER {
     ~DIGITAL_FILTER()
     {
         DFSharedStream &ss = df_shared_stream();
-        if (ss.last == this) ss.last = nullptr; // the state stays published
+        if (ss.last == this) { // publish the state before the handle that holds it goes
+            try {
+                ss.materialize();
+            } catch (...) {
+            }
+            ss.last = nullptr;
+            ss.last_h = nullptr;
+        }
+        unpin_all();
         df_destroy(h_);
     }
 
@@ -259,16 +325,19 @@ class DIGITAL_FILTER {
     {
         DFSharedStream &ss = df_shared_stream();
         if (!cfg_.shared_stream || !ss.seeded || ss.last == this) return;
+        ss.materialize();
         check(df_set_rng_state(h_, ss.state, ss.saved_flag, ss.saved));
         ss.last = this;
+        ss.last_h = h_;
     }
-    void stream_out()
+    void stream_out() // this handle now holds the process's stream; read back lazily (materialize)
     {
         if (!cfg_.shared_stream) return;
         DFSharedStream &ss = df_shared_stream();
-        check(df_rng_state(h_, &ss.state, &ss.saved_flag, &ss.saved));
         ss.seeded = true;
+        ss.stale = true;
         ss.last = this;
+        ss.last_h = h_;
     }
     // Host mirrors of the setup (rows, scalars, vertices, half-widths) and of step 0's fields.
     void mirror_setup()
@@ -307,7 +376,7 @@ class DIGITAL_FILTER {
         fill_field(w, 2);
         rho_fluc.assign(n_cells, 0.0);
         T_fluc.assign(n_cells, 0.0);
-        refresh();
+        refresh_full();
     }
 
   public:
@@ -340,12 +409,12 @@ class DIGITAL_FILTER {
     void apply_RST_scaling()
     {
         check(df_apply_RST_scaling(h_));
-        refresh();
+        refresh_full();
     }
     void get_rho_T_fluc()
     {
         check(df_get_rho_T_fluc(h_));
-        refresh();
+        refresh_full();
     }
     void filter(double dt_input)
     {
@@ -510,6 +579,9 @@ class DIGITAL_FILTER {
 
     // ====== MI355X extensions
     df_handle *handle() { return h_; }
+    // Refresh every host mirror now (filt_old and filt included), whatever host_mirror says.
+    void sync_host() { refresh_mirrors(true); }
+    void set_host_mirror(int level) { cfg_.host_mirror = level; }
     const double *device_field(int which) { return df_device_field(h_, which); } // zero-copy for a GPU CFD
     const Vector &T_fluc_host() const { return T_fluc; }
     const Vector &rho_fluc_host() const { return rho_fluc; }
@@ -553,6 +625,6 @@ class DIGITAL_FILTER {
         check(df_set_field(h_, DF_FILT_OLD_U, ck.filt_old_u.data()));
         check(df_set_field(h_, DF_FILT_OLD_V, ck.filt_old_v.data()));
         check(df_set_field(h_, DF_FILT_OLD_W, ck.filt_old_w.data()));
-        refresh();
+        refresh_full();
     }
 };

@@ -100,7 +100,8 @@ typedef struct df_profile {
 
 /* Reference defaults (df.cpp:7-16) plus: coeff_mode DF_COEFF_TABLE (bit-identical to
  * DF_COEFF_PACKED, no coefficient stream), vel_fluc_file / line_file = the profiles in
- * df_data_dir(). */
+ * df_data_dir(). (The Python test/bench mirror dfamd.make_config defaults to DF_COEFF_PACKED,
+ * the reference's data contract; its docstring lists what the mode changes besides the bytes.) */
 void df_config_default(df_config_c *cfg);
 /* The data/ directory next to the loaded libdfamd.so (RST.dat, line.dat). */
 const char *df_data_dir(void);
@@ -130,6 +131,19 @@ int df_get_rho_T_fluc(df_handle *h);                /* df.cpp:470-485 */
 
 /* Host copy of a dense [Ny x Nz_local] field (u.fluc etc., df.hpp:24-34). Synchronizes. */
 int df_get_field(df_handle *h, int which, double *host_out);
+/* Several fields at once (the drop-in's per-call host mirrors): host_out[i] receives field which[i];
+ * all copies are queued on the handle's stream and the call synchronizes ONCE. */
+int df_get_fields(df_handle *h, int n, const int *which, double *const *host_out);
+/* Process-wide registry of the library's live device allocations, every handle's. Each allocation is
+ * checked against it: one that overlaps a live range fails (df_create returns NULL, DF_EHIP, the
+ * message names both ranges) instead of silently aliasing another handle's buffer. Diagnostic entry:
+ * claim (claim = 1) or release (claim = 0) a range by hand; df_alloc_registry_count = live ranges. */
+int df_alloc_registry(const void *p, size_t bytes, int claim);
+long long df_alloc_registry_count(void);
+/* Page-lock caller memory (hipHostRegister) so df_get_field(s) into it run as DMA transfers;
+ * df_host_unpin releases it (call before the memory is freed). */
+int df_host_pin(void *p, size_t bytes);
+int df_host_unpin(void *p);
 /* Upload a dense [Ny x Nz_local] host field into which = DF_U..DF_FILT_OLD_W. Synchronizes.
  * Checkpoint/resume: the reference's resumable state is the stream (df_rng_state)
  * plus filt_old of u, v, w (df.cpp:440-442); df_set_rng_state + df_set_field(DF_FILT_OLD_*)
@@ -198,7 +212,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * "zunroll" (2,4), "nt_stores", "rng_nt_stores", "zstage" (table z-pass noise staged in LDS: 0 off, 1 element copy,
  * 2 16-B copy with its loads issued first, the default),
  * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "fuse_plan" (planes of
- * <= 1024 attempt blocks: K3 plans its own waves, one launch fewer; default 1 in table mode), "graph" (steady-state
+ * <= 1024 attempt blocks: K3 plans its own waves, one launch fewer; default 1 in table mode and on packed
+ * planes without long y chains, 0 on packed planes that use the row-pair y-pass), "graph" (steady-state
  * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
@@ -213,10 +228,12 @@ double df_algorithmic_bytes(df_handle *h, int kernel /* -1 whole call, 0 ypass, 
 int df_comm_unique_id(void *out, size_t len); /* RCCL unique id, len >= 128 */
 
 /* What one df_filter of a z-strip handle exchanges (bench and monitoring).
- * rccl_ranks comes from ncclCommCount on the handle's communicator (0: no RCCL). With the
- * default replicated counting the halo send/recv is the call's only collective
- * (rng_collective 0); df_set_tuning(h, "rng_replicate", 0) switches to split counting plus one
- * all-gather of block counts, wave counts and accept masks per call (rng_collective 1). */
+ * rccl_ranks comes from ncclCommCount on the handle's communicator (0: no RCCL). The collective
+ * form follows coeff_mode: DF_COEFF_PACKED replicates the counting, so the halo send/recv is the
+ * call's only collective (rng_collective 0); DF_COEFF_TABLE (the df_config_default mode) splits the
+ * counting and adds one all-gather of block and wave accept counts per call (rng_collective 1) - only
+ * counts travel, K3 recomputes the accept flags of the waves it runs. df_set_tuning(h,
+ * "rng_replicate", 0 | 1) overrides either default (alike on every rank, before the first df_filter). */
 typedef struct df_comm_stats {
     int rccl_ranks, rccl_rank;    /* ncclCommCount / ncclCommUserRank; 0, 0 without RCCL */
     int halo_peers;               /* neighbours this strip exchanges z-halo columns with (0-2) */

@@ -568,6 +568,30 @@ def test_checkpoint_restore_continues_bitexact():
         b.set_field("filt_old_u", np.zeros(5))
 
 
+def test_alloc_registry_tracks_live_handles():
+    """The process-wide registry holds every live device range of every handle: a range inside a live
+    handle's buffer is refused (DF_EHIP, both ranges named), and destroying the handle releases all
+    of its ranges (an allocation aliasing another handle's buffer fails loudly)."""
+    import ctypes as C
+    L = dfamd.lib()
+    L.df_alloc_registry.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    L.df_alloc_registry_count.restype = C.c_longlong
+    L.df_device_field.restype = C.c_void_p
+    n0 = L.df_alloc_registry_count()
+    a = gpu_synth(96, 140, 2, 12, seed=5)
+    na = L.df_alloc_registry_count()
+    assert na > n0
+    b = gpu_synth(96, 140, 2, 12, seed=6, coeff_mode="table")
+    assert L.df_alloc_registry_count() > na
+    p = L.df_device_field(a._h, 3)  # a's T' buffer
+    assert L.df_alloc_registry(p + 64, 64, 1) == -3
+    assert "overlaps the live range" in L.df_last_error().decode()
+    b.close()
+    assert L.df_alloc_registry_count() == na
+    a.close()
+    assert L.df_alloc_registry_count() == n0
+
+
 # ---------------------------------------------------------------- randomized sweep of shapes
 
 def _random_cases(n=10, seed=20261015):

@@ -142,6 +142,12 @@ def test_c_abi_rejects_bad_arguments():
     assert L.df_set_tuning(f._h, b"bogus", 2) == -1
     assert b"unknown tuning" in L.df_last_error()
     assert L.df_set_tuning(f._h, b"rows_per_wave", 2) == 0
+    # launch-shape keys that rebalance device tile lists must not touch the absent device state
+    # (a host-only handle never built its tap ranges)
+    for key in (b"ycoop_ovh", b"ycoop"):
+        assert L.df_set_tuning(f._h, key, 7) == 0
+    native = host()  # the reference's grid: long y chains, the row-pair plan
+    assert L.df_set_tuning(native._h, b"ycoop_ovh", 64) == 0
     cfg, keep = dfamd.make_config(device=-1, seed=1, coeff_mode="packed")
     cfg.coeff_mode = 7
     assert not L.df_create(C.byref(cfg))
@@ -279,3 +285,29 @@ def test_grid_plane_strips_partition_coefficients(world):
             assert np.array_equal(np.concatenate([s.halfwidths(c, d) for s in strips], axis=1),
                                   whole.halfwidths(c, d))
         assert sum(s.comp_info(c)["by_size"] for s in strips) == whole.comp_info(c)["by_size"]
+
+
+def test_alloc_registry_rejects_overlapping_ranges():
+    """every device allocation of every handle is checked against the live ranges
+    of all handles; an overlap fails with DF_EHIP naming both ranges (fed synthetic ranges here)."""
+    import ctypes as C
+    L = dfamd.lib()
+    L.df_alloc_registry.argtypes = [C.c_void_p, C.c_size_t, C.c_int]
+    L.df_alloc_registry_count.restype = C.c_longlong
+    base = 0x7f0000000000  # far from any host or device mapping of this process; never dereferenced
+    n0 = L.df_alloc_registry_count()
+    assert L.df_alloc_registry(base, 0x1000, 1) == 0
+    assert L.df_alloc_registry(base + 0x1000, 0x1000, 1) == 0  # adjacent: no overlap
+    assert L.df_alloc_registry_count() == n0 + 2
+    for start, size in ((base + 0x800, 0x1000),    # straddles the first range's end
+                        (base - 0x10, 0x20),        # straddles the first range's start
+                        (base + 0x100, 0x10),       # inside
+                        (base - 0x1000, 0x4000)):   # covers both
+        assert L.df_alloc_registry(start, size, 1) == -3  # DF_EHIP
+        msg = L.df_last_error().decode()
+        assert "overlaps the live range" in msg and hex(start) in msg, msg
+    assert L.df_alloc_registry_count() == n0 + 2  # a refused claim is not recorded
+    assert L.df_alloc_registry(base, 0, 0) == 0 and L.df_alloc_registry(base + 0x1000, 0, 0) == 0
+    assert L.df_alloc_registry_count() == n0
+    assert L.df_alloc_registry(base + 0x800, 0x1000, 1) == 0  # free again after release
+    assert L.df_alloc_registry(base + 0x800, 0, 0) == 0

@@ -202,13 +202,25 @@ DF_HD double log_r2(double x, const LogTabEntry *tab)
 // constants of glibc_log_table.h; it returns glibc's bits for every argument tested
 // (tests/test_rng_log.py: 1e8 uniform doubles in (0, 1], the near-1 band, powers of two), so the
 // normals, and with them the fields, are bit-identical to the reference's.
+// glibc's near-1 band: ix - LO < HI - LO (x in [1 - 2^-4, 1 + 0x1.09p-4)); 6.25% of the polar r2.
+constexpr uint64_t kGlNearLo = 0x3FEE000000000000ull; // asuint64(1.0 - 0x1p-4)
+constexpr uint64_t kGlNearHi = 0x3FF1090000000000ull; // asuint64(1.0 + 0x1.09p-4)
+DF_HD bool glibc_log_near1(double x) { return dbits(x) - kGlNearLo < kGlNearHi - kGlNearLo; }
+
+// The two halves of glibc_log below, for callers that sort their arguments by band first (the dense
+// noise generation defers near-1 lanes into batches of their own, so neither half diverges).
+DF_HD double glibc_log_band1(double x);
+DF_HD double glibc_log_main(double x);
+
 DF_HD double glibc_log(double x)
 {
-    const uint64_t ix = dbits(x);
-    constexpr uint64_t LO = 0x3FEE000000000000ull; // asuint64(1.0 - 0x1p-4)
-    constexpr uint64_t HI = 0x3FF1090000000000ull; // asuint64(1.0 + 0x1.09p-4)
-    if (ix - LO < HI - LO) { // close to 1
-        if (ix == 0x3FF0000000000000ull) return 0.0;
+    return glibc_log_near1(x) ? glibc_log_band1(x) : glibc_log_main(x);
+}
+
+DF_HD double glibc_log_band1(double x)
+{
+    {
+        if (dbits(x) == 0x3FF0000000000000ull) return 0.0;
         const double r = x - 1.0;
         const double r2 = r * r;
         const double r3 = r * r2;
@@ -226,6 +238,11 @@ DF_HD double glibc_log(double x)
         y += hi;
         return y;
     }
+}
+
+DF_HD double glibc_log_main(double x)
+{
+    const uint64_t ix = dbits(x);
     constexpr uint64_t OFF = 0x3FE6000000000000ull;
     const uint64_t tmp = ix - OFF;
     const int i = (int)((tmp >> 45) & 127);

@@ -59,7 +59,7 @@ static int time_dropin(char **argv)
               << ", \"capi_ms\": " << capi << ", \"capi_async_ms\": " << capi_async
               << ", \"dropin_ms\": {\"mirror0\": " << dropin[0] << ", \"mirror1\": " << dropin[1]
               << ", \"mirror2\": " << dropin[2] << "}, \"mirror_bytes\": {\"mirror1\": " << 5 * 8 * cells
-              << ", \"mirror2\": " << 8 * 8 * cells << "}}" << std::endl;
+              << ", \"mirror2\": " << 11 * 8 * cells << "}}" << std::endl;
     return 0;
 }
 

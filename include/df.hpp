@@ -181,7 +181,7 @@ class DIGITAL_FILTER {
         size_t bytes = 0;
         const void *refused = nullptr; // the runtime refused this buffer: do not retry every call
     };
-    Pin pins_[8];
+    Pin pins_[11];
     void pin(Vector &v, Pin &pn)
     {
         v.resize(n_cells);
@@ -199,23 +199,22 @@ class DIGITAL_FILTER {
             if (pn.p) df_host_unpin(const_cast<void *>(pn.p));
         for (Pin &pn : pins_) pn = Pin{};
     }
-    // Every mirror in one df_get_fields: one stream synchronisation per refresh.
+    // Every mirror in one df_get_fields: one stream synchronisation per refresh. After apply_RST_scaling
+    // the reference's filt equals filt_old (df.cpp:440-442): filt is a second DMA copy of the device
+    // filt_old (at PCIe rate, ~2x faster than copying the host vector).
     void refresh_mirrors(bool with_filt_old)
     {
-        Vector *dst[8] = {&u.fluc, &v.fluc, &w.fluc, &T_fluc, &rho_fluc, &u.filt_old, &v.filt_old, &w.filt_old};
-        const int which[8] = {DF_U, DF_V, DF_W, DF_T, DF_RHO, DF_FILT_OLD_U, DF_FILT_OLD_V, DF_FILT_OLD_W};
-        const int n = with_filt_old ? 8 : 5;
-        double *out[8];
+        Vector *dst[11] = {&u.fluc,     &v.fluc,     &w.fluc, &T_fluc, &rho_fluc, &u.filt_old,
+                           &v.filt_old, &w.filt_old, &u.filt, &v.filt, &w.filt};
+        const int which[11] = {DF_U,          DF_V,          DF_W,          DF_T,          DF_RHO,       DF_FILT_OLD_U,
+                               DF_FILT_OLD_V, DF_FILT_OLD_W, DF_FILT_OLD_U, DF_FILT_OLD_V, DF_FILT_OLD_W};
+        const int n = with_filt_old ? 11 : 5;
+        double *out[11];
         for (int i = 0; i < n; ++i) {
             pin(*dst[i], pins_[i]);
             out[i] = dst[i]->data();
         }
         check(df_get_fields(h_, n, which, out));
-        if (with_filt_old) { // after apply_RST_scaling the reference's filt equals filt_old (df.cpp:440-442)
-            u.filt = u.filt_old;
-            v.filt = v.filt_old;
-            w.filt = w.filt_old;
-        }
     }
     void refresh() // after filter() / get_rms(): the per-call set
     {

@@ -104,6 +104,11 @@ struct df_handle {
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
     int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
+    // Dense generation (RngGeom::gen_dense: compaction through memory, one wave per needed 64-rank chunk,
+    // near-1 log lanes deferred). Default in table mode (VALU-bound, where K3's skeleton costs); packed
+    // keeps the compacted K3 (its RNG hides under the HBM-bound sweeps; the dense form adds 2 x 8 B per
+    // stored pair of traffic). Never on planes that use fused_plan or gen_split > 1 (small planes).
+    int gen_dense = 0;
     int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
     // table y-pass: noise and coefficients loaded a whole 4-tap group ahead (ypass_kernel): c3 y-pass
     // 0.141 -> 0.133 ms alone, the reference's grid and c2 -4.5% per call (profiles/r2/ab_ydeep_table.jsonl)
@@ -385,6 +390,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
+    g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? 1 : 0;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
@@ -759,6 +765,9 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_ZSPLIT")) h->zsplit = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE || h->ycoop < 7 ? 1 : 0;
+    if (const char *e = std::getenv("DFAMD_FUSE_PLAN")) h->fuse_plan = std::atoi(e);
+    h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
+    if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -1120,6 +1129,69 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
     return upload(h, h->rstate, &st0, 1);
 }
 
+// Dense generation tables (RngGeom::gen_dense): for each parity f of the incoming cached normal, the
+// 64-rank chunks whose pairs (positions f + 2r, f + 2r + 1) store something on this GPU - the same
+// columns as stream_dest: r_ys columns [z0, z1), r_zs pads on the plane's first/last strip - plus the
+// chunk of the call's last rank A - 1 (it sets the stream state). Bitmap for Kc, list for K3a.
+int alloc_dense(df_handle *h)
+{
+    const RngGeom &g = h->geom;
+    const uint64_t A0 = (g.Q + 1) / 2; // A for f = 0 (f = 1: A0 or A0 - 1)
+    const uint64_t nch = (A0 + 63) / 64;
+    if (nch >= (1ull << 31)) return fail(DF_EINVAL, "plane too large for the dense generation tables");
+    std::vector<uint32_t> bits[2], list[2];
+    for (int f = 0; f < 2; ++f) {
+        bits[f].assign((nch + 31) / 32, 0u);
+        const long long A = (long long)((g.Q - f + 1) / 2);
+        auto mark = [&](uint64_t qa, uint64_t qb) { // positions [qa, qb)
+            if (qb <= qa || qb < (uint64_t)f + 1) return;
+            const long long r0 = qa > (uint64_t)f ? (long long)((qa - f) / 2) : 0;
+            long long r1 = (long long)((qb - 1 - f) / 2); // inclusive
+            if (r1 > A - 1) r1 = A - 1;
+            for (long long c = r0 >> 6; c <= (r1 >> 6); ++c) bits[f][c >> 5] |= 1u << (c & 31);
+        };
+        for (int sidx = 0; sidx < 6; ++sidx) {
+            const uint64_t base = g.seg[sidx], W = g.width[sidx], rows = g.rows[sidx];
+            const int cmp = sidx >> 1;
+            if ((sidx & 1) == 0) { // r_ys: this strip's columns of every row
+                if (g.z0 == 0 && (uint64_t)g.z1 == W) mark(base, base + rows * W);
+                else
+                    for (uint64_t r = 0; r < rows; ++r) mark(base + r * W + g.z0, base + r * W + g.z1);
+            } else { // r_zs: the raw-noise pads (df.cpp:343-348) on the plane's edge strips
+                const uint64_t nzp = (uint64_t)g.Nzp[cmp];
+                for (uint64_t r = 0; r < rows; ++r) {
+                    if (g.is_first) mark(base + r * W, base + r * W + nzp);
+                    if (g.is_last) mark(base + r * W + nzp + g.Nz_g, base + (r + 1) * W);
+                }
+            }
+        }
+        if (A > 0) bits[f][((A - 1) >> 6) >> 5] |= 1u << (((A - 1) >> 6) & 31);
+        for (uint64_t c = 0; c < nch; ++c)
+            if ((bits[f][c >> 5] >> (c & 31)) & 1u) list[f].push_back((uint32_t)c);
+    }
+    int rc;
+    uint32_t *db[2], *dl[2];
+    for (int f = 0; f < 2; ++f) {
+        if ((rc = dalloc_t(h, &db[f], bits[f].size()))) return rc;
+        if ((rc = upload(h, db[f], bits[f].data(), bits[f].size()))) return rc;
+        if ((rc = dalloc_t(h, &dl[f], std::max<size_t>(1, list[f].size())))) return rc;
+        if (!list[f].empty() && (rc = upload(h, dl[f], list[f].data(), list[f].size()))) return rc;
+        h->geom.need_bits[f] = db[f];
+        h->geom.chunks[f] = dl[f];
+        h->geom.nchunks[f] = (int)list[f].size();
+    }
+    // near-1 queue: 12.5% of the needed ranks (glibc's band holds 6.25% of r2); a full queue makes K3a
+    // evaluate the rest in place, so the bound only affects speed
+    const size_t needed = (size_t)std::max(list[0].size(), list[1].size()) * 64;
+    h->geom.near_cap = (int)std::min<size_t>(std::max<size_t>(needed / 8, 4096), 1u << 30);
+    if ((rc = dalloc_t(h, &h->geom.near_q, (size_t)h->geom.near_cap))) return rc;
+    if ((rc = dalloc_t(h, &h->geom.near_count, 1))) return rc;
+    uint64_t *cs = nullptr;
+    if ((rc = dalloc_t(h, &cs, nch * 64))) return rc;
+    h->geom.cstate = cs;
+    return DF_OK;
+}
+
 // Halo buffers and the RCCL communicators (cfg->comm_id).
 int open_comm(df_handle *h, const df_config_c *cfg)
 {
@@ -1155,6 +1227,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = upload_tables(h))) return rc;
     if ((rc = alloc_components(h))) return rc;
     if ((rc = alloc_rng(h, cfg))) return rc;
+    if (h->gen_dense && h->geom.gen_split == 1 && (rc = alloc_dense(h))) return rc;
     if ((rc = open_comm(h, cfg))) return rc;
     for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
@@ -1802,6 +1875,13 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
+    else if (k == "gen_dense") {
+        if (value && h->device >= 0 && !h->geom.cstate) {
+            int rc = alloc_dense(h);
+            if (rc) return rc;
+        }
+        h->gen_dense = value != 0;
+    }
     else if (k == "fast_log") {
         if (value < 0 || value > 2) return fail(DF_EINVAL, "fast_log must be 0 (device log), 1 (log_r2) or 2 (glibc_log)");
         h->geom.fast_log = value;

@@ -747,6 +747,207 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     }
 }
 
+// ---------------------------------------------------------------- dense generation (gen_dense)
+//
+// The compacted K3 above spends more time in its per-wave skeleton (ring appends, batch loop, per-lane
+// destination walk, mostly scalar and branch work: 29M SALU against 37M VALU per c3 table call) than in
+// the transform. The dense form moves the compaction through memory instead:
+//   Kc  one wave per attempt wave: its first rank from the scan, its accept flags (K1's masks or the
+//       screen recomputed), and for each accepted attempt whose 64-rank chunk stores something here the
+//       attempt's start state into cstate[rank] (consecutive ranks: coalesced 8-B stores);
+//   K3a one wave per needed chunk (host-built list for the call's parity f), lane l = rank 64c + l:
+//       the state from cstate, the four draws, the transform, the pair's destination by arithmetic
+//       (consecutive lanes, consecutive 16-B pairs). Every lane busy but the partial chunks at the pad
+//       edges; no skipped batches, no ring. glibc's near-1 band (6.25% of r2, so in 98% of 64-lane
+//       batches) is not evaluated here: those lanes append (x, y, rank) to near_q;
+//   K3b the near-1 entries, dense: the near-1 half of glibc_log alone.
+// Same draws, same arithmetic (x*x + y*y and the log's band test are recomputed bit for bit), same
+// destinations as K3: bit-identical noise.
+
+__device__ __forceinline__ bool chunk_needed(const uint32_t *bits, long long c)
+{
+    return (bits[c >> 5] >> (c & 31)) & 1u;
+}
+
+__global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                       const long long *__restrict__ offsets,
+                                                                       const long long *__restrict__ part,
+                                                                       const int *__restrict__ wave_counts,
+                                                                       const uint16_t *__restrict__ masks,
+                                                                       int nb_total)
+{
+    constexpr int WPB = kRngThreads / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int b = blockIdx.x, gw = b * WPB + w;
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    if (gw == 0 && lane == 0) {
+        *g.near_count = 0; // K3a of this generation appends after this kernel has completed
+        if (f) {           // the normal cached by the previous call is stream position 0 (random.tcc:1809)
+            double *d = stream_dest(g, stream_pos(g, 0));
+            if (d) *d = sin->saved * 1.0 + 0.0;
+        }
+    }
+    if (b >= nb_total) return;
+    long long r_lo = offsets[b] + part[b >> 10];
+    for (int ww = 0; ww < w; ++ww) r_lo += wave_counts[(size_t)b * WPB + ww];
+    r_lo = __builtin_amdgcn_readfirstlane((int)(r_lo >> 32)) * 4294967296ll +
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r_lo); // uniform
+    if (r_lo >= A) return;
+    const long long r_end = min(r_lo + (long long)wave_counts[gw], A); // this wave's ranks [r_lo, r_end)
+    const uint32_t *nb = g.need_bits[f];
+    bool any = false;
+    for (long long c = r_lo >> 6; c <= ((r_end - 1) >> 6) && !any; ++c) any = chunk_needed(nb, c);
+    if (!any) return;
+    const int tid = w * 64 + lane;
+    const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
+    uint64_t st = thread_first_state(g, sin->state, b, tid);
+    long long R = r_lo; // uniform: rank of this iteration's first accepted attempt
+#pragma unroll 4
+    for (int m = 0; m < kRngPerThread; ++m) {
+        const bool acc = (bits >> m) & 1u;
+        const uint64_t mask = __ballot(acc);
+        const int n = __popcll(mask);
+        if (n && R < A) {
+            const long long c0 = R >> 6, c1 = (R + n - 1) >> 6; // at most two chunks per iteration
+            const bool n0 = chunk_needed(nb, c0), n1 = c1 != c0 && chunk_needed(nb, c1);
+            if (n0 || n1) {
+                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+                const long long rank = R + below;
+                if (acc && rank < A && ((rank >> 6) == c0 ? n0 : n1)) g.cstate[rank] = st;
+            }
+        }
+        R += n;
+        st = g.next_mult * st + g.next_plus;
+    }
+}
+
+// Destination of stream position q inside a chunk whose first position P0 is known (uniform): the
+// chunk spans 128 positions of one array with rows of >= 128 normals, so at most one row wrap.
+__device__ __forceinline__ double *dense_dest(const RngGeom &g, int su, uint32_t row, uint32_t col)
+{
+    const StreamPos p{su, row, col};
+    return stream_dest(g, p);
+}
+
+__device__ __forceinline__ void store_pair(const RngGeom &g, double *d0, double *d1, double n0, double n1)
+{
+    if (g.debug_flags & 2) {
+        if (n0 == 1234.5) *d0 = n1; // keep the values alive
+    } else if (d0 && d1 == d0 + 1 && ((uintptr_t)d0 & 15) == 0) {
+        if (g.nt_stores) __builtin_nontemporal_store(dvec2{n0, n1}, reinterpret_cast<dvec2 *>(d0));
+        else *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
+    } else {
+        if (d0) *d0 = n0;
+        if (d1) *d1 = n1;
+    }
+}
+
+__global__ __launch_bounds__(kRngThreads) void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                        RngStateDev *__restrict__ sout)
+{
+    const int lane = threadIdx.x & 63;
+    const int i = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    if (i >= g.nchunks[f]) return;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    const long long c = (long long)uniform((int)g.chunks[f][i]);
+    const long long rank = c * 64 + lane;
+    const uint64_t q = f + 2ull * (uint64_t)rank;
+    const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform
+    const StreamPos P0 = stream_pos(g, q0);
+    const int su = P0.sidx < 6 ? P0.sidx : 5;
+    const uint32_t W = g.width[su];
+    const bool generic = P0.sidx >= 6 || W < 128 || q0 + 128 > g.seg[su + 1];
+    double *d0 = nullptr, *d1 = nullptr;
+    const bool live = rank < A;
+    if (live) {
+        if (!generic) {
+            uint32_t row = P0.row, col = P0.col + 2u * (uint32_t)lane;
+            if (col >= W) {
+                col -= W;
+                ++row;
+            }
+            d0 = dense_dest(g, su, row, col);
+            if (++col == W) {
+                col = 0;
+                ++row;
+            }
+            d1 = dense_dest(g, su, row, col); // q + 1 < the array's end (q0 + 128 <= seg[su + 1])
+        } else {
+            const StreamPos p0 = stream_pos(g, q);
+            d0 = stream_dest(g, p0);
+            d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
+        }
+    }
+    const bool last = live && rank == A - 1;
+    if (!(d0 || d1 || last)) return;
+    uint64_t s3 = g.cstate[rank];
+    PolarAttempt a;
+    if (g.debug_flags & 4) {
+        a.x = (double)(uint32_t)s3 * 1e-10;
+        a.y = 0.5;
+        a.r2 = 0.5;
+    } else {
+        a = polar_draws(s3, s3); // the draws K1 tested; s3 left at the fourth output's state
+    }
+    double lg;
+    if (g.fast_log == 2) {
+        bool near = glibc_log_near1(a.r2);
+        bool inline_near = near && last; // the call's last attempt also sets the stream state: never deferred
+        const uint64_t dm = __ballot(near && !last);
+        if (dm) {
+            const int cnt = __popcll(dm);
+            int base = 0;
+            if (lane == __builtin_ctzll(dm)) base = atomicAdd(g.near_count, cnt);
+            base = __shfl(base, __builtin_ctzll(dm));
+            if (base + cnt <= g.near_cap) {
+                if (near && !last) {
+                    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+                    g.near_q[base + below] = Near1Entry{a.x, a.y, rank, 0.0};
+                    return;
+                }
+            } else {
+                inline_near = near; // queue full (never expected): evaluate here, same bits
+            }
+        }
+        lg = __ballot(inline_near) ? glibc_log(a.r2) : glibc_log_main(a.r2);
+    } else {
+        lg = polar_log(g, a.r2);
+    }
+    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * lg / a.r2);
+    const double xm = a.x * mult;
+    const double ym = a.y * mult;
+    store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+    if (last) {
+        sout->state = s3 * kPcgMult + kPcgInc; // state after this attempt's 4th output
+        sout->saved_flag = (int)((g.Q - f) & 1u);
+        sout->saved = xm;
+    }
+}
+
+__global__ __launch_bounds__(256) void rng_dense_near1_kernel(RngGeom g, const RngStateDev *__restrict__ sin)
+{
+    const int n = *g.near_count < g.near_cap ? *g.near_count : g.near_cap;
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
+        const Near1Entry d = g.near_q[e];
+        const double xx = d.x * d.x; // polar_draws' r2, bit for bit
+        const double yy = d.y * d.y;
+        const double r2 = xx + yy;
+        const double mult = (g.debug_flags & 1) ? r2 : sqrt(-2 * glibc_log_band1(r2) / r2);
+        const double xm = d.x * mult;
+        const double ym = d.y * mult;
+        const uint64_t q = f + 2ull * (uint64_t)d.rank;
+        const StreamPos p0 = stream_pos(g, q);
+        double *d0 = stream_dest(g, p0);
+        double *d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
+        store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+    }
+}
+
 // K2 + K2c in one block for planes of at most 1024 attempt blocks (c1, c2, the reference's own
 // grid): the scan of the block counts (one count per thread), the attempt-shortage check and the
 // wave plan, with the offsets kept in LDS. One launch instead of three: small planes are bound by
@@ -836,6 +1037,23 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 #else
     constexpr bool small_ok = true;
 #endif
+    if (g.gen_dense) {
+        if (small_ok && nb_scan <= 1024 && nb_total <= 1024)
+            hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
+                               wave_counts, nb_scan, 0, tasks, ntasks, err); // scan only (no plan: nb_total 0)
+        else {
+            hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
+            hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err, ntasks);
+        }
+        hipLaunchKernelGGL(rng_dense_compact_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, offsets, part,
+                           wave_counts, masks, nb_total);
+        const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
+        hipLaunchKernelGGL(rng_dense_generate_kernel, dim3((nch + 3) / 4), dim3(kRngThreads), 0, st, g, st_in, st_out);
+        int nq = (g.near_cap + 255) / 256;
+        nq = nq < 1 ? 1 : (nq > 1024 ? 1024 : nq);
+        hipLaunchKernelGGL(rng_dense_near1_kernel, dim3(nq), dim3(256), 0, st, g, st_in);
+        return hipGetLastError();
+    }
     if (g.fused_plan && g.gen_compact) {
         // the compacted K3 plans its own waves (small planes: one launch fewer per call)
     } else if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {

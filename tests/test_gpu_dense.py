@@ -1,0 +1,98 @@
+"""Dense noise generation (RngGeom::gen_dense, round 3: Kc compacts the accepted attempts' states into
+memory by rank, K3a runs one wave per needed 64-rank chunk, K3b evaluates glibc's near-1 log band
+apart). It is the table-mode default on planes of more than 1024 attempt blocks and on split planes;
+here it is forced on small planes (DFAMD_GEN_DENSE=1, DFAMD_GEN_SPLIT=1, DFAMD_FUSE_PLAN=0 at create)
+and checked bit for bit against the oracle: fields, the stream state after every call, the six noise
+arrays, both parities of the carried normal (f = 0 and a resumed f = 1), z-strip groups, and packed
+mode."""
+import numpy as np
+import pytest
+
+import dfamd
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("u", "v", "w", "T", "rho")
+
+
+@pytest.fixture
+def dense_env(monkeypatch):
+    monkeypatch.setenv("DFAMD_GEN_DENSE", "1")
+    monkeypatch.setenv("DFAMD_GEN_SPLIT", "1")
+    monkeypatch.setenv("DFAMD_FUSE_PLAN", "0")
+
+
+def synth(Ny, Nz, lo, hi, **kw):
+    return dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=lo, N_max=hi, device=0, **kw)
+
+
+def start_state(seed, flag):
+    """A stream state with the cached-normal flag f = flag (f = 1 shifts every pair by one position)."""
+    st = O.pcg32_seed1(seed)
+    return (st, flag, 0.7734375 if flag else 0.0)
+
+
+@pytest.mark.parametrize("flag", [0, 1])
+@pytest.mark.parametrize("mode", ["table", "packed"])
+@pytest.mark.parametrize("spec", [(128, 128, 8, 8), (37, 5, 2, 10), (70, 129, 2, 6), (96, 300, 4, 20), (2, 1, 2, 2)])
+def test_dense_fields_bitexact_vs_oracle(dense_env, spec, mode, flag):
+    st = start_state(3 + flag, flag)
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3],
+                 rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))
+    g = synth(*spec, resume=st, coeff_mode=mode)
+    for dt in (None, 1e-8, 1e-8, 1e-5):
+        if dt is not None:
+            o.filter(dt)
+            g.filter(dt)
+        gf, of = g.fields(), o.fields()
+        for k in FIELDS:
+            assert np.array_equal(gf[k], of[k]), (dt, k, float(np.abs(gf[k] - of[k]).max()))
+        assert g.rng_state() == o.rng.state, dt
+
+
+@pytest.mark.parametrize("flag", [0, 1])
+def test_dense_noise_arrays_bitexact(dense_env, flag):
+    spec = (64, 200, 2, 12)
+    st = start_state(11, flag)
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=64, Nz=200, N_min=2, N_max=12,
+                 rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))
+    g = synth(*spec, resume=st, coeff_mode="table")
+    for _ in range(2):
+        o.filter(1e-8)
+        g.filter(1e-8)
+    for c in range(3):
+        F = o.comp(c)
+        ry_o = np.ctypeslib.as_array(F.r_ys, shape=(F.r_ys_size,)).reshape(-1, o.Nz)
+        assert np.array_equal(g.noise(c, "y"), ry_o), c
+        rz_o = np.ctypeslib.as_array(F.r_zs, shape=(F.r_zs_size,)).reshape(o.Ny, -1)
+        assert np.array_equal(g.noise(c, "z"), rz_o), c
+
+
+@pytest.mark.parametrize("world,Nz", [(2, 300), (3, 700)])
+def test_dense_strip_groups_match_whole(dense_env, world, Nz):
+    spec = dict(plane="synthetic", Ny=100, Nz=Nz, N_min=4, N_max=16, seed=8, device=0, coeff_mode="table")
+    whole = dfamd.DigitalFilter(**spec)
+    strips = dfamd.create_group(world, **spec)
+    for _ in range(3):
+        whole.filter(1e-8)
+        dfamd.filter_group(strips, 1e-8)
+    for k in FIELDS:
+        cat = np.concatenate([s.field(k) for s in strips], axis=1)
+        assert np.array_equal(cat, whole.field(k)), k
+    assert all(s.rng_state() == whole.rng_state() for s in strips)
+
+
+def test_dense_and_compact_forms_agree_when_switched():
+    # the default table plane switched between the dense and the compacted K3 between calls
+    spec = (200, 300, 4, 24)
+    a = synth(*spec, seed=21, coeff_mode="table")
+    b = synth(*spec, seed=21, coeff_mode="table")
+    for kw in (dict(fuse_plan=0, gen_split=1, gen_dense=1), dict(gen_dense=0), dict(gen_dense=1),
+               dict(fuse_plan=1, gen_dense=1), dict(fuse_plan=0, gen_split=2, gen_dense=1)):
+        for k, v in kw.items():
+            b.set_tuning(k, v)
+        a.filter(1e-8)
+        b.filter(1e-8)
+        for k in FIELDS:
+            assert np.array_equal(a.field(k), b.field(k)), (kw, k)
+        assert a.rng_state() == b.rng_state(), kw

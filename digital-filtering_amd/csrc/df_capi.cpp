@@ -1141,7 +1141,7 @@ int alloc_dense(df_handle *h)
     if (nch >= (1ull << 31)) return fail(DF_EINVAL, "plane too large for the dense generation tables");
     std::vector<uint32_t> bits[2], list[2];
     for (int f = 0; f < 2; ++f) {
-        bits[f].assign((nch + 31) / 32, 0u);
+        bits[f].assign((nch + 31) / 32 + 2, 0u); // + 2 padding words: Kc reads a 64-bit window
         const long long A = (long long)((g.Q - f + 1) / 2);
         auto mark = [&](uint64_t qa, uint64_t qb) { // positions [qa, qb)
             if (qb <= qa || qb < (uint64_t)f + 1) return;
@@ -1180,12 +1180,6 @@ int alloc_dense(df_handle *h)
         h->geom.chunks[f] = dl[f];
         h->geom.nchunks[f] = (int)list[f].size();
     }
-    // near-1 queue: 12.5% of the needed ranks (glibc's band holds 6.25% of r2); a full queue makes K3a
-    // evaluate the rest in place, so the bound only affects speed
-    const size_t needed = (size_t)std::max(list[0].size(), list[1].size()) * 64;
-    h->geom.near_cap = (int)std::min<size_t>(std::max<size_t>(needed / 8, 4096), 1u << 30);
-    if ((rc = dalloc_t(h, &h->geom.near_q, (size_t)h->geom.near_cap))) return rc;
-    if ((rc = dalloc_t(h, &h->geom.near_count, 1))) return rc;
     uint64_t *cs = nullptr;
     if ((rc = dalloc_t(h, &cs, nch * 64))) return rc;
     h->geom.cstate = cs;

@@ -755,19 +755,16 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
 //   Kc  one wave per attempt wave: its first rank from the scan, its accept flags (K1's masks or the
 //       screen recomputed), and for each accepted attempt whose 64-rank chunk stores something here the
 //       attempt's start state into cstate[rank] (consecutive ranks: coalesced 8-B stores);
-//   K3a one wave per needed chunk (host-built list for the call's parity f), lane l = rank 64c + l:
-//       the state from cstate, the four draws, the transform, the pair's destination by arithmetic
-//       (consecutive lanes, consecutive 16-B pairs). Every lane busy but the partial chunks at the pad
-//       edges; no skipped batches, no ring. glibc's near-1 band (6.25% of r2, so in 98% of 64-lane
-//       batches) is not evaluated here: those lanes append (x, y, rank) to near_q;
-//   K3b the near-1 entries, dense: the near-1 half of glibc_log alone.
-// Same draws, same arithmetic (x*x + y*y and the log's band test are recomputed bit for bit), same
+//   K3a one wave per kDenseG needed chunks (host-built list for the call's parity f), lane l of chunk c =
+//       rank 64c + l: the state from cstate (the next chunk's loaded while this one computes), the four
+//       draws, the transform, the pair's destination by arithmetic (consecutive lanes, consecutive 16-B
+//       pairs). Every lane busy but the partial chunks at the pad edges; no skipped batches, no ring.
+//       glibc's near-1 band (6.25% of r2, so present in 98% of 64-lane batches) is not evaluated in the
+//       chunk's batch: those lanes push (x, y, destinations) on a wave-private LDS stack, popped 64 at a
+//       time into batches of their own (the near-1 half of glibc_log alone), the rest at the wave's end.
+// Same draws, same arithmetic (x*x + y*y and the log's band test recomputed bit for bit), same
 // destinations as K3: bit-identical noise.
-
-__device__ __forceinline__ bool chunk_needed(const uint32_t *bits, long long c)
-{
-    return (bits[c >> 5] >> (c & 31)) & 1u;
-}
+constexpr int kDenseG = 8; // chunks per K3a wave
 
 __global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                        const long long *__restrict__ offsets,
@@ -777,28 +774,29 @@ __global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom 
                                                                        int nb_total)
 {
     constexpr int WPB = kRngThreads / 64;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
     const int b = blockIdx.x, gw = b * WPB + w;
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
-    if (gw == 0 && lane == 0) {
-        *g.near_count = 0; // K3a of this generation appends after this kernel has completed
-        if (f) {           // the normal cached by the previous call is stream position 0 (random.tcc:1809)
-            double *d = stream_dest(g, stream_pos(g, 0));
-            if (d) *d = sin->saved * 1.0 + 0.0;
-        }
+    if (gw == 0 && lane == 0 && f) { // the normal cached by the previous call is stream position 0
+        double *d = stream_dest(g, stream_pos(g, 0));
+        if (d) *d = sin->saved * 1.0 + 0.0;
     }
     if (b >= nb_total) return;
-    long long r_lo = offsets[b] + part[b >> 10];
-    for (int ww = 0; ww < w; ++ww) r_lo += wave_counts[(size_t)b * WPB + ww];
-    r_lo = __builtin_amdgcn_readfirstlane((int)(r_lo >> 32)) * 4294967296ll +
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r_lo); // uniform
-    if (r_lo >= A) return;
-    const long long r_end = min(r_lo + (long long)wave_counts[gw], A); // this wave's ranks [r_lo, r_end)
-    const uint32_t *nb = g.need_bits[f];
-    bool any = false;
-    for (long long c = r_lo >> 6; c <= ((r_end - 1) >> 6) && !any; ++c) any = chunk_needed(nb, c);
-    if (!any) return;
+    // the block's offset and its four waves' counts, loaded together
+    const long long ob = offsets[b] + part[b >> 10];
+    const int4 wc = *reinterpret_cast<const int4 *>(wave_counts + (size_t)b * WPB);
+    const long long r_lo = ob + (w > 0 ? wc.x : 0) + (w > 1 ? wc.y : 0) + (w > 2 ? wc.z : 0);
+    const int nw = w == 0 ? wc.x : w == 1 ? wc.y : w == 2 ? wc.z : wc.w;
+    if (r_lo >= A || nw == 0) return;
+    const long long r_end = min(r_lo + (long long)nw, A); // this wave's ranks [r_lo, r_end)
+    // needed bits of the wave's chunks [c_lo, c_hi] (<= 17 of them): one 64-bit window of the bitmap
+    const long long c_lo = r_lo >> 6, c_hi = (r_end - 1) >> 6;
+    const uint32_t *nb = g.need_bits[f] + (c_lo >> 5); // the bitmap has two padding words
+    const uint64_t win = ((uint64_t)nb[0] | ((uint64_t)nb[1] << 32)) >> (c_lo & 31);
+    const int span = (int)(c_hi - c_lo); // < 32
+    const uint32_t need = (uint32_t)win & ((2u << span) - 1u);
+    if (!need) return;
     const int tid = w * 64 + lane;
     const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
     uint64_t st = thread_first_state(g, sin->state, b, tid);
@@ -808,27 +806,18 @@ __global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom 
         const bool acc = (bits >> m) & 1u;
         const uint64_t mask = __ballot(acc);
         const int n = __popcll(mask);
-        if (n && R < A) {
-            const long long c0 = R >> 6, c1 = (R + n - 1) >> 6; // at most two chunks per iteration
-            const bool n0 = chunk_needed(nb, c0), n1 = c1 != c0 && chunk_needed(nb, c1);
-            if (n0 || n1) {
+        if (n && R < r_end) {
+            const int k0 = (int)((R >> 6) - c_lo), k1 = (int)(((R + n - 1) >> 6) - c_lo); // <= 2 chunks
+            if ((need >> k0) & (0xFFFFFFFFu >> (31 - (k1 - k0)))) {
                 const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
                 const long long rank = R + below;
-                if (acc && rank < A && ((rank >> 6) == c0 ? n0 : n1)) g.cstate[rank] = st;
+                if (acc && rank < A && ((need >> ((rank >> 6) - c_lo)) & 1u)) g.cstate[rank] = st;
             }
         }
         R += n;
         st = g.next_mult * st + g.next_plus;
     }
-}
-
-// Destination of stream position q inside a chunk whose first position P0 is known (uniform): the
-// chunk spans 128 positions of one array with rows of >= 128 normals, so at most one row wrap.
-__device__ __forceinline__ double *dense_dest(const RngGeom &g, int su, uint32_t row, uint32_t col)
-{
-    const StreamPos p{su, row, col};
-    return stream_dest(g, p);
 }
 
 __device__ __forceinline__ void store_pair(const RngGeom &g, double *d0, double *d1, double n0, double n1)
@@ -844,107 +833,127 @@ __device__ __forceinline__ void store_pair(const RngGeom &g, double *d0, double 
     }
 }
 
+// A deferred near-1 lane: its uniforms and its two destinations (nullptr: not stored here).
+struct Near1Slot {
+    double x, y;
+    double *d0, *d1;
+};
+
+// Pop n <= 64 deferred near-1 lanes from the top of the wave's stack and finish them: x*x + y*y is
+// polar_draws' r2 bit for bit, and every argument is in glibc's near-1 band.
+__device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q, int top, int n, int lane)
+{
+    if (lane >= n) return;
+    const Near1Slot e = q[top - n + lane];
+    const double xx = e.x * e.x;
+    const double yy = e.y * e.y;
+    const double r2 = xx + yy;
+    const double mult = (g.debug_flags & 1) ? r2 : sqrt(-2 * glibc_log_band1(r2) / r2);
+    const double xm = e.x * mult;
+    const double ym = e.y * mult;
+    store_pair(g, e.d0, e.d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+}
+
 __global__ __launch_bounds__(kRngThreads) void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                         RngStateDev *__restrict__ sout)
 {
-    const int lane = threadIdx.x & 63;
-    const int i = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
+    __shared__ Near1Slot stack_all[kRngThreads / 64][128]; // < 64 carried + 64 pushed per chunk
+    const int lane = threadIdx.x & 63, wv = uniform(threadIdx.x >> 6);
+    Near1Slot *stk = stack_all[wv];
     const uint64_t f = (uint64_t)sin->saved_flag;
-    if (i >= g.nchunks[f]) return;
+    const int nch = g.nchunks[f];
+    const int i0 = (blockIdx.x * (kRngThreads / 64) + wv) * kDenseG;
+    if (i0 >= nch) return;
+    const int ng = min(kDenseG, nch - i0);
     const long long A = (long long)((g.Q - f + 1) / 2);
-    const long long c = (long long)uniform((int)g.chunks[f][i]);
-    const long long rank = c * 64 + lane;
-    const uint64_t q = f + 2ull * (uint64_t)rank;
-    const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform
-    const StreamPos P0 = stream_pos(g, q0);
-    const int su = P0.sidx < 6 ? P0.sidx : 5;
-    const uint32_t W = g.width[su];
-    const bool generic = P0.sidx >= 6 || W < 128 || q0 + 128 > g.seg[su + 1];
-    double *d0 = nullptr, *d1 = nullptr;
-    const bool live = rank < A;
-    if (live) {
-        if (!generic) {
-            uint32_t row = P0.row, col = P0.col + 2u * (uint32_t)lane;
-            if (col >= W) {
-                col -= W;
-                ++row;
-            }
-            d0 = dense_dest(g, su, row, col);
-            if (++col == W) {
-                col = 0;
-                ++row;
-            }
-            d1 = dense_dest(g, su, row, col); // q + 1 < the array's end (q0 + 128 <= seg[su + 1])
-        } else {
-            const StreamPos p0 = stream_pos(g, q);
-            d0 = stream_dest(g, p0);
-            d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
-        }
-    }
-    const bool last = live && rank == A - 1;
-    if (!(d0 || d1 || last)) return;
-    uint64_t s3 = g.cstate[rank];
-    PolarAttempt a;
-    if (g.debug_flags & 4) {
-        a.x = (double)(uint32_t)s3 * 1e-10;
-        a.y = 0.5;
-        a.r2 = 0.5;
-    } else {
-        a = polar_draws(s3, s3); // the draws K1 tested; s3 left at the fourth output's state
-    }
-    double lg;
-    if (g.fast_log == 2) {
-        bool near = glibc_log_near1(a.r2);
-        bool inline_near = near && last; // the call's last attempt also sets the stream state: never deferred
-        const uint64_t dm = __ballot(near && !last);
-        if (dm) {
-            const int cnt = __popcll(dm);
-            int base = 0;
-            if (lane == __builtin_ctzll(dm)) base = atomicAdd(g.near_count, cnt);
-            base = __shfl(base, __builtin_ctzll(dm));
-            if (base + cnt <= g.near_cap) {
-                if (near && !last) {
-                    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-                    g.near_q[base + below] = Near1Entry{a.x, a.y, rank, 0.0};
-                    return;
+    const uint32_t *lst = g.chunks[f] + i0;
+    const bool defer = g.fast_log == 2;
+    int top = 0; // uniform stack height
+    long long c = uniform((int)lst[0]);
+    uint64_t s = c * 64 + lane < A ? g.cstate[c * 64 + lane] : 0;
+    for (int k = 0; k < ng; ++k) {
+        // the next chunk's states are in flight while this chunk computes
+        const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
+        const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
+        const long long rank = c * 64 + lane;
+        const uint64_t q = f + 2ull * (uint64_t)rank;
+        const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform
+        const StreamPos P0 = stream_pos(g, q0);
+        const int su = P0.sidx < 6 ? P0.sidx : 5;
+        const uint32_t W = g.width[su];
+        const bool generic = P0.sidx >= 6 || W < 128 || q0 + 128 > g.seg[su + 1];
+        double *d0 = nullptr, *d1 = nullptr;
+        const bool live = rank < A;
+        if (live) {
+            if (!generic) { // one array, at most one row wrap
+                uint32_t row = P0.row, col = P0.col + 2u * (uint32_t)lane;
+                if (col >= W) {
+                    col -= W;
+                    ++row;
                 }
+                d0 = stream_dest(g, StreamPos{su, row, col});
+                if (++col == W) {
+                    col = 0;
+                    ++row;
+                }
+                d1 = stream_dest(g, StreamPos{su, row, col}); // q + 1 < the array's end
             } else {
-                inline_near = near; // queue full (never expected): evaluate here, same bits
+                const StreamPos p0 = stream_pos(g, q);
+                d0 = stream_dest(g, p0);
+                d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
             }
         }
-        lg = __ballot(inline_near) ? glibc_log(a.r2) : glibc_log_main(a.r2);
-    } else {
-        lg = polar_log(g, a.r2);
+        const bool last = live && rank == A - 1;
+        const bool active = d0 || d1 || last;
+        PolarAttempt a{};
+        uint64_t s3 = s;
+        bool near = false;
+        if (active) {
+            if (g.debug_flags & 4) {
+                a.x = (double)(uint32_t)s * 1e-10;
+                a.y = 0.5;
+                a.r2 = 0.5;
+            } else {
+                a = polar_draws(s, s3); // the draws K1 tested; s3 left at the fourth output's state
+            }
+            // the call's last attempt also sets the stream state: never deferred
+            near = defer && !last && glibc_log_near1(a.r2);
+        }
+        const uint64_t nm = __ballot(near);
+        if (nm) {
+            if (near) {
+                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nm >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)nm, 0u));
+                stk[top + below] = Near1Slot{a.x, a.y, d0, d1};
+            }
+            top += __popcll(nm);
+        }
+        if (active && !near) {
+            double lg;
+            if (defer) lg = __ballot(last && glibc_log_near1(a.r2)) ? glibc_log(a.r2) : glibc_log_main(a.r2);
+            else lg = polar_log(g, a.r2);
+            const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * lg / a.r2);
+            const double xm = a.x * mult;
+            const double ym = a.y * mult;
+            store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+            if (last) {
+                sout->state = s3 * kPcgMult + kPcgInc; // state after this attempt's 4th output
+                sout->saved_flag = (int)((g.Q - f) & 1u);
+                sout->saved = xm;
+            }
+        }
+        if (top >= 64) { // the stack is wave-private and a wave's LDS ops complete in order
+            __asm__ volatile("" ::: "memory");
+            near1_batch(g, stk, top, 64, lane);
+            top -= 64;
+            __asm__ volatile("" ::: "memory");
+        }
+        c = cn;
+        s = sn;
     }
-    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * lg / a.r2);
-    const double xm = a.x * mult;
-    const double ym = a.y * mult;
-    store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
-    if (last) {
-        sout->state = s3 * kPcgMult + kPcgInc; // state after this attempt's 4th output
-        sout->saved_flag = (int)((g.Q - f) & 1u);
-        sout->saved = xm;
-    }
-}
-
-__global__ __launch_bounds__(256) void rng_dense_near1_kernel(RngGeom g, const RngStateDev *__restrict__ sin)
-{
-    const int n = *g.near_count < g.near_cap ? *g.near_count : g.near_cap;
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n; e += gridDim.x * blockDim.x) {
-        const Near1Entry d = g.near_q[e];
-        const double xx = d.x * d.x; // polar_draws' r2, bit for bit
-        const double yy = d.y * d.y;
-        const double r2 = xx + yy;
-        const double mult = (g.debug_flags & 1) ? r2 : sqrt(-2 * glibc_log_band1(r2) / r2);
-        const double xm = d.x * mult;
-        const double ym = d.y * mult;
-        const uint64_t q = f + 2ull * (uint64_t)d.rank;
-        const StreamPos p0 = stream_pos(g, q);
-        double *d0 = stream_dest(g, p0);
-        double *d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
-        store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+    if (top > 0) {
+        __asm__ volatile("" ::: "memory");
+        near1_batch(g, stk, top, top, lane);
     }
 }
 
@@ -1048,10 +1057,9 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_dense_compact_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, offsets, part,
                            wave_counts, masks, nb_total);
         const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
-        hipLaunchKernelGGL(rng_dense_generate_kernel, dim3((nch + 3) / 4), dim3(kRngThreads), 0, st, g, st_in, st_out);
-        int nq = (g.near_cap + 255) / 256;
-        nq = nq < 1 ? 1 : (nq > 1024 ? 1024 : nq);
-        hipLaunchKernelGGL(rng_dense_near1_kernel, dim3(nq), dim3(256), 0, st, g, st_in);
+        const int per_block = kDenseG * (kRngThreads / 64);
+        hipLaunchKernelGGL(rng_dense_generate_kernel, dim3((nch + per_block - 1) / per_block), dim3(kRngThreads), 0, st,
+                           g, st_in, st_out);
         return hipGetLastError();
     }
     if (g.fused_plan && g.gen_compact) {

@@ -48,13 +48,6 @@ struct WaveTask {
     int gw, pad;
 };
 
-// A deferred near-1 lane of the dense generation (K3a -> K3b): its uniforms and its rank.
-struct Near1Entry {
-    double x, y;
-    long long rank;
-    double pad;
-};
-
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
@@ -80,16 +73,13 @@ struct RngGeom {
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];
     // Dense generation (gen_dense): Kc writes the start state of every accepted attempt whose 64-rank
-    // chunk stores something here to cstate[rank]; K3a runs one wave per such chunk (the host's list for
-    // the call's parity f = incoming saved_flag), a lane per rank; glibc's near-1 lanes go to near_q for K3b.
+    // chunk stores something here to cstate[rank]; K3a runs a wave per 8 such chunks (the host's list for
+    // the call's parity f = incoming saved_flag), a lane per rank.
     int gen_dense;
     uint64_t *cstate;               // [64 * chunk count]
-    const uint32_t *need_bits[2];   // bitmap over chunks, per parity f
+    const uint32_t *need_bits[2];   // bitmap over chunks (+ 2 padding words), per parity f
     const uint32_t *chunks[2];      // needed chunk ids in increasing order, per parity f
     int nchunks[2];
-    Near1Entry *near_q;             // [near_cap]
-    int *near_count;
-    int near_cap;
 };
 
 struct SweepArgs {

@@ -179,6 +179,28 @@ def test_c4_eight_z_strips_table_match_single():
     assert all(s.rng_state() == whole.rng_state() for s in strips)
 
 
+@pytest.mark.parametrize("mode", ["table", "packed"])
+def test_c5_eight_z_strips_match_single(mode):
+    """c5 (BASELINE configs[4]: 4096 x 4096, N 4-64) split the way the 8-GPU bench splits it: eight
+    z-strips of 512 columns in one process (device-to-device halo and count copies in place of the RCCL
+    calls), against the whole plane run unsplit in table mode, bit for bit. Packed strips hold the
+    85 GB coefficient stream between them."""
+    spec = dict(plane="synthetic", seed=406, device=0, Ny=4096, Nz=4096, N_min=4, N_max=64)
+    whole = dfamd.DigitalFilter(coeff_mode="table", **spec)
+    strips = dfamd.create_group(8, coeff_mode=mode, **spec)
+    assert [s.Nz_loc for s in strips] == [512] * 8
+    for _ in range(2):
+        whole.filter(1e-8)
+        dfamd.filter_group(strips, 1e-8)
+    for k in ("u", "v", "w", "T", "rho"):
+        cat = np.concatenate([s.field(k) for s in strips], axis=1)
+        assert np.array_equal(cat, whole.field(k)), k
+    assert all(s.rng_state() == whole.rng_state() for s in strips)
+    for s in strips:
+        s.close()
+    whole.close()
+
+
 def test_c5_full_size_sampled_rows():
     """c5 (4096 x 4096, N 4-64): 85 GB of offset-packed coefficients on one GPU; the
     Sigma(2N+1) = 1.7e9 offsets exceed nothing (64-bit on the device)."""

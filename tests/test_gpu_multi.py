@@ -84,8 +84,8 @@ def check_world(outs, world, replicate, Nz=1024):
         assert c["halo_peers"] == (0 if world == 1 else (1 if o["rank"] in (0, world - 1) else 2))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 1), ("table", 0)])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 1), ("table", 0), ("packed", 0)])
 def test_rccl_strips_emulated_hosts(world, mode, replicate):
     """world ranks on one GPU, one emulated host each: the peer send/recv path on a one-GPU box."""
     if n_gpus() < 1:

@@ -76,6 +76,22 @@ module df_c_binding
             integer(c_int), value :: which
             real(c_double), intent(out) :: out(*)
         end function
+        integer(c_int) function df_get_fields(h, n, which, host_out) bind(C, name="df_get_fields")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+            integer(c_int), value :: n
+            integer(c_int), intent(in) :: which(*)
+            type(c_ptr), intent(in) :: host_out(*)
+        end function
+        integer(c_int) function df_host_pin(p, bytes) bind(C, name="df_host_pin")
+            import :: c_ptr, c_int, c_size_t
+            type(c_ptr), value :: p
+            integer(c_size_t), value :: bytes
+        end function
+        integer(c_int) function df_host_unpin(p) bind(C, name="df_host_unpin")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: p
+        end function
         type(c_ptr) function df_device_field(h, which) bind(C, name="df_device_field")
             import :: c_ptr, c_int
             type(c_ptr), value :: h
@@ -230,6 +246,7 @@ module DIGITAL_FILTERING
         real(kind=dp) :: dt = 0.0_dp
         real(kind=dp) :: u_tau = 0.0_dp, tau_w = 0.0_dp
         logical :: host_mirror = .true., on_device = .true.
+        type(c_ptr) :: pinned(8) = c_null_ptr       ! page-locked mirror buffers (df_host_pin), by address
         type(FilterField) :: u, v, w
         real(kind=dp), allocatable :: T_fluc(:), rho_fluc(:)
         real(kind=dp), allocatable :: R11(:), R21(:), R22(:), R33(:), yc(:)
@@ -388,20 +405,37 @@ contains
         end select
     end function field_of
 
-    ! Host mirrors of the current fields (one D2H copy each; skipped when host_mirror = .false.).
+    ! Host mirrors of the current fields: the eight D2H copies queued together, one synchronisation
+    ! (df_get_fields), into page-locked arrays (re-registered if an array moved, e.g. after the
+    ! assignment df = create_digital_filter(...)); skipped when host_mirror = .false.
     subroutine refresh(DF)
         type(digital_filter_type), intent(inout), target :: DF
-        integer :: comp
+        integer :: comp, i
         type(FilterField), pointer :: F
+        integer(c_int) :: which(8), rc
+        type(c_ptr) :: outp(8)
         do comp = 0, 2
             F => field_of(DF, comp)
             if (.not. allocated(F%fluc)) allocate(F%fluc(DF%n_cells), F%filt_old(DF%n_cells))
-            call check(df_get_field(DF%handle, int(comp, c_int), F%fluc), 'df_get_field')
-            call check(df_get_field(DF%handle, int(DF_FILT_OLD_U + comp, c_int), F%filt_old), 'df_get_field')
+            which(comp + 1) = int(comp, c_int)
+            outp(comp + 1) = c_loc(F%fluc)
+            which(comp + 4) = int(DF_FILT_OLD_U + comp, c_int)
+            outp(comp + 4) = c_loc(F%filt_old)
         end do
         if (.not. allocated(DF%T_fluc)) allocate(DF%T_fluc(DF%n_cells), DF%rho_fluc(DF%n_cells))
-        call check(df_get_field(DF%handle, DF_T, DF%T_fluc), 'df_get_field')
-        call check(df_get_field(DF%handle, DF_RHO, DF%rho_fluc), 'df_get_field')
+        which(7) = DF_T
+        outp(7) = c_loc(DF%T_fluc)
+        which(8) = DF_RHO
+        outp(8) = c_loc(DF%rho_fluc)
+        do i = 1, 8
+            if (.not. c_associated(outp(i), DF%pinned(i))) then
+                if (c_associated(DF%pinned(i))) rc = df_host_unpin(DF%pinned(i))
+                DF%pinned(i) = c_null_ptr
+                ! a refused registration leaves a pageable copy (slower, same bytes)
+                if (df_host_pin(outp(i), int(DF%n_cells, c_size_t) * 8_c_size_t) == DF_OK) DF%pinned(i) = outp(i)
+            end if
+        end do
+        call check(df_get_fields(DF%handle, 8_c_int, which, outp), 'df_get_fields')
     end subroutine refresh
 
     ! filter(DF, dt) (df.f90:621-651 shape; df.cpp:449-468 semantics).
@@ -415,6 +449,12 @@ contains
 
     subroutine destroy_digital_filter(DF)
         type(digital_filter_type), intent(inout) :: DF
+        integer :: i
+        integer(c_int) :: rc
+        do i = 1, 8
+            if (c_associated(DF%pinned(i))) rc = df_host_unpin(DF%pinned(i))
+            DF%pinned(i) = c_null_ptr
+        end do
         if (c_associated(DF%handle)) call df_destroy(DF%handle)
         DF%handle = c_null_ptr
     end subroutine destroy_digital_filter

@@ -832,6 +832,7 @@ int plan_rng(df_handle *h)
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
     g.gen_compact = 1;
+    g.dense_g = 8;
     g.fast_log = 2; // glibc's own log in the polar transform: normals bit-identical (tests/test_rng_log.py)
     if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
@@ -1869,6 +1870,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
+    else if (k == "dense_g") {
+        if (value != 4 && value != 8 && value != 16) return fail(DF_EINVAL, "dense_g must be 4, 8 or 16");
+        h->geom.dense_g = value;
+    }
     else if (k == "gen_dense") {
         if (value && h->device >= 0 && !h->geom.cstate) {
             int rc = alloc_dense(h);

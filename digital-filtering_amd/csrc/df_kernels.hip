@@ -764,7 +764,6 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
 //       time into batches of their own (the near-1 half of glibc_log alone), the rest at the wave's end.
 // Same draws, same arithmetic (x*x + y*y and the log's band test recomputed bit for bit), same
 // destinations as K3: bit-identical noise.
-constexpr int kDenseG = 8; // chunks per K3a wave
 
 __global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                        const long long *__restrict__ offsets,
@@ -854,6 +853,7 @@ __device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q
     store_pair(g, e.d0, e.d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
 }
 
+template <int kDenseG> // chunks per K3a wave (RngGeom::dense_g: 4, 8 or 16)
 __global__ __launch_bounds__(kRngThreads) void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                         RngStateDev *__restrict__ sout)
 {
@@ -1057,9 +1057,12 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_dense_compact_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, offsets, part,
                            wave_counts, masks, nb_total);
         const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
-        const int per_block = kDenseG * (kRngThreads / 64);
-        hipLaunchKernelGGL(rng_dense_generate_kernel, dim3((nch + per_block - 1) / per_block), dim3(kRngThreads), 0, st,
-                           g, st_in, st_out);
+        const int per_block = g.dense_g * (kRngThreads / 64);
+        const dim3 grid((nch + per_block - 1) / per_block);
+        if (g.dense_g == 4) hipLaunchKernelGGL(rng_dense_generate_kernel<4>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
+        else if (g.dense_g == 16)
+            hipLaunchKernelGGL(rng_dense_generate_kernel<16>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
+        else hipLaunchKernelGGL(rng_dense_generate_kernel<8>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
         return hipGetLastError();
     }
     if (g.fused_plan && g.gen_compact) {

@@ -104,6 +104,9 @@ def parse(argv=None):
                    help="filter(dt) calls of the long run (device get_rms accumulation every call, steady-state "
                         "and total time, the SURVEY 4 variance invariant at the end); auto: 10000 on c5 at N > 1 "
                         "(BASELINE configs[4]), else none; an integer K runs K calls on the main workload")
+    p.add_argument("--profile-every", type=int, default=4,
+                   help="phase events (hipEventRecord) on every n-th timed call only: on calls of 0.1-0.2 ms six "
+                        "events per call cost 1-10%% of the wall time (tools/event_cost.py)")
     p.add_argument("--dry-run", action="store_true",
                    help="launch plumbing only: every rank reports its env, rank 0 prints one JSON line; no GPU")
     p.add_argument("--dropin", default="auto", choices=["auto", "off"],
@@ -347,7 +350,7 @@ def timed(ctx, h, args, min_warm_s=0.0, profile=True, collective=True):
             h.filter(args.dt)
             calls += 1
         h.sync()
-    h.set_profiling(profile)
+    h.set_profiling(profile, every=args.profile_every if args.steps >= 2 * args.profile_every else 1)
     if collective:
         ctx.barrier()
     torch.cuda.synchronize()

@@ -167,6 +167,9 @@ struct df_handle {
     long long rms_count = 0;
     // profiling
     bool profiling = false;
+    int profile_every = 1;  // events on every profile_every-th df_filter only (df_set_profiling(h, n))
+    long long prof_seq = 0; // df_filter calls since profiling was switched on
+    bool prof_call = false; // this df_filter records its phase events
     std::vector<PhaseEvents> ev;
     size_t ev_used = 0;
     df_profile prof{};
@@ -337,7 +340,7 @@ int check_rng_error(df_handle *h)
     return DF_OK;
 }
 
-bool prof_on(df_handle *h) { return h->profiling && h->ev_used < h->ev.size(); }
+bool prof_on(df_handle *h) { return h->profiling && h->prof_call && h->ev_used < h->ev.size(); }
 
 void ev_record(df_handle *h, int phase)
 {
@@ -1507,6 +1510,9 @@ int df_filter(df_handle *h, double dt)
         return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     if (graph_ok(h)) return graph_call(h, dt);
+    // Sampled phase events: each hipEventRecord is a queue packet between this call's kernels, and on
+    // short calls six of them cost up to 10% of the call (tools/event_cost.py; profiles/r3/d)
+    h->prof_call = h->profiling && (h->prof_seq++ % h->profile_every) == 0;
     const bool prof = prof_on(h);
     if ((rc = consume_gen(h))) return rc;
     ev_record(h, 0);
@@ -1518,6 +1524,7 @@ int df_filter(df_handle *h, double dt)
     ev_record(h, 3);
     if ((rc = prefetch_gen(h))) return rc; // next call's noise, under this call's sweeps
     if (prof) h->ev_used++;
+    h->prof_call = false;
     return write_csv_if(h);
 }
 
@@ -1912,8 +1919,11 @@ int df_set_profiling(df_handle *h, int on)
         for (auto &pe : h->ev)
             for (auto &e : pe.e) HIP_OR(hipEventCreate(&e), DF_EHIP);
     }
+    if (on < 0) return fail(DF_EINVAL, "df_set_profiling: on must be >= 0");
     int rc = drain_profile(h);
     h->profiling = on != 0;
+    h->profile_every = on > 1 ? on : 1;
+    h->prof_seq = 0;
     h->prof = df_profile{};
     return rc;
 }

@@ -375,8 +375,9 @@ class DigitalFilter:
     def set_tuning(self, key, value):
         _check(lib().df_set_tuning(self._h, key.encode(), int(value)))
 
-    def set_profiling(self, on):
-        _check(lib().df_set_profiling(self._h, 1 if on else 0))
+    def set_profiling(self, on, every=1):
+        """on: phase events on; every n > 1: only on every n-th filter() call (sampled)."""
+        _check(lib().df_set_profiling(self._h, max(1, int(every)) if on else 0))
 
     def profile(self):
         p = Profile()

@@ -217,7 +217,9 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
-/* Timing (hipEvents on the handle's stream). */
+/* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every
+ * n-th df_filter only (the first of each n; df_profile.calls counts the timed calls): the events are
+ * queue packets between a call's kernels and cost up to 10% of a short call. */
 int df_set_profiling(df_handle *h, int on);
 int df_get_profile(df_handle *h, df_profile *out);
 int df_sync(df_handle *h);

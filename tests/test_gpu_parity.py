@@ -676,3 +676,24 @@ def test_handles_driven_from_two_host_threads():
         for k in FIELDS:
             assert np.array_equal(f.field(k), r[k]), k
         f.close()
+
+
+def test_sampled_profiling_counts_and_phases():
+    # df_set_profiling(h, n): phase events on every n-th call only (bench.py --profile-every)
+    f = gpu_synth(64, 200, 2, 12, seed=3)
+    a = gpu_synth(64, 200, 2, 12, seed=3)
+    f.set_profiling(True, every=4)
+    for _ in range(12):
+        f.filter(1e-8)
+        a.filter(1e-8)
+    p = f.profile()
+    assert p["calls"] == 3
+    assert p["ypass_ms"] > 0 and p["zpass_ms"] > 0 and p["total_ms"] >= p["zpass_ms"]
+    f.set_profiling(True)
+    for _ in range(5):
+        f.filter(1e-8)
+        a.filter(1e-8)
+    assert f.profile()["calls"] == 5
+    f.set_profiling(False)
+    for k in FIELDS:  # events never change a result
+        assert np.array_equal(f.field(k), a.field(k)), k

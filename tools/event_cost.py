@@ -26,17 +26,17 @@ else:
 for _ in range(50):
     f.filter(1e-8)
 f.sync()
-res = {"off": [], "on": []}
+res = {"off": [], "on": [], "every4": []}
 for _ in range(rounds):
-    for k in ("off", "on"):
-        f.set_profiling(k == "on")
+    for k in res:
+        f.set_profiling(k != "off", every=4 if k == "every4" else 1)
         f.sync()
         t0 = time.perf_counter()
         for _ in range(calls):
             f.filter(1e-8)
         f.sync()
         res[k].append((time.perf_counter() - t0) * 1e3 / calls)
-        if k == "on":
+        if k != "off":
             f.profile()
 print(json.dumps({"config": cfg, "mode": mode, "calls": calls,
                   "ms_per_call_median": {k: round(statistics.median(v), 4) for k, v in res.items()},

@@ -836,6 +836,7 @@ int plan_rng(df_handle *h)
     }
     g.gen_compact = 1;
     g.dense_g = 8;
+    g.count_grid = 0;
     g.fast_log = 2; // glibc's own log in the polar transform: normals bit-identical (tests/test_rng_log.py)
     if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
@@ -1877,8 +1878,13 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
+    else if (k == "count_grid") {
+        if (value < 0) return fail(DF_EINVAL, "count_grid must be >= 0");
+        h->geom.count_grid = value;
+    }
     else if (k == "dense_g") {
-        if (value != 4 && value != 8 && value != 16) return fail(DF_EINVAL, "dense_g must be 4, 8 or 16");
+        if (value != 4 && value != 8 && value != 16 && value != 32 && value != 128)
+            return fail(DF_EINVAL, "dense_g must be 4, 8, 16, 32 or 128");
         h->geom.dense_g = value;
     }
     else if (k == "gen_dense") {

@@ -143,31 +143,35 @@ __device__ __forceinline__ uint32_t lane_accept_bits(const RngGeom &g, uint64_t 
 
 // Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
 // the last z-strip rank's share) report zero.
+// Blocks [b0, b0 + nb) with a grid of gridDim.x <= nb blocks striding over them (RngGeom::count_grid
+// caps how many K1 waves are resident beside the sweeps; 0 = one block per attempt block).
 __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                int *__restrict__ counts, int *__restrict__ wave_counts,
-                                                               uint16_t *__restrict__ masks, int b0, int nb_total)
+                                                               uint16_t *__restrict__ masks, int b0, int nb, int nb_total)
 {
     __shared__ int wsum[kRngThreads / 64];
     const int tid = threadIdx.x, w = tid >> 6;
-    const int gb = b0 + blockIdx.x;
-    if (gb >= nb_total) {
-        if (tid == 0) counts[gb] = 0;
-        if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
-        return;
-    }
-    const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
-    int cnt = __builtin_popcount(bits);
-    masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if ((tid & 63) == 0) {
-        wsum[w] = cnt;
-        wave_counts[(size_t)gb * (kRngThreads / 64) + w] = cnt; // the wave's run of 1024 attempts
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int t = 0;
-        for (int ww = 0; ww < kRngThreads / 64; ++ww) t += wsum[ww];
-        counts[gb] = t;
+    for (int gb = b0 + blockIdx.x; gb < b0 + nb; gb += gridDim.x) { // block-uniform trip count
+        if (gb >= nb_total) {
+            if (tid == 0) counts[gb] = 0;
+            if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
+            continue;
+        }
+        const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
+        int cnt = __builtin_popcount(bits);
+        masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if ((tid & 63) == 0) {
+            wsum[w] = cnt;
+            wave_counts[(size_t)gb * (kRngThreads / 64) + w] = cnt; // the wave's run of 1024 attempts
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int ww = 0; ww < kRngThreads / 64; ++ww) t += wsum[ww];
+            counts[gb] = t;
+        }
+        __syncthreads(); // wsum is rewritten by the next iteration
     }
 }
 
@@ -1031,8 +1035,9 @@ __global__ __launch_bounds__(1024) void rng_scan_plan_small_kernel(RngGeom g, co
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
-    hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
-                       nb_total);
+    const int grid = g.count_grid > 0 && g.count_grid < nb ? g.count_grid : nb;
+    hipLaunchKernelGGL(rng_count_kernel, dim3(grid), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
+                       nb, nb_total);
     return hipGetLastError();
 }
 
@@ -1059,10 +1064,15 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
         const int per_block = g.dense_g * (kRngThreads / 64);
         const dim3 grid((nch + per_block - 1) / per_block);
-        if (g.dense_g == 4) hipLaunchKernelGGL(rng_dense_generate_kernel<4>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
-        else if (g.dense_g == 16)
-            hipLaunchKernelGGL(rng_dense_generate_kernel<16>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
-        else hipLaunchKernelGGL(rng_dense_generate_kernel<8>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
+        switch (g.dense_g) {
+        case 4: hipLaunchKernelGGL(rng_dense_generate_kernel<4>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
+        case 16: hipLaunchKernelGGL(rng_dense_generate_kernel<16>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
+        case 32: hipLaunchKernelGGL(rng_dense_generate_kernel<32>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
+        case 128:
+            hipLaunchKernelGGL(rng_dense_generate_kernel<128>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
+            break;
+        default: hipLaunchKernelGGL(rng_dense_generate_kernel<8>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
+        }
         return hipGetLastError();
     }
     if (g.fused_plan && g.gen_compact) {

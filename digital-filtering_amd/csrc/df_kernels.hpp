@@ -76,7 +76,8 @@ struct RngGeom {
     // chunk stores something here to cstate[rank]; K3a runs a wave per 8 such chunks (the host's list for
     // the call's parity f = incoming saved_flag), a lane per rank.
     int gen_dense;
-    int dense_g;                    // needed chunks per K3a wave: 4, 8 (default) or 16
+    int dense_g;                    // needed chunks per K3a wave: 4, 8 (default), 16, 32, 128
+    int count_grid;                 // K1 blocks (striding over the attempt blocks); 0 = one per attempt block
     uint64_t *cstate;               // [64 * chunk count]
     const uint32_t *need_bits[2];   // bitmap over chunks (+ 2 padding words), per parity f
     const uint32_t *chunks[2];      // needed chunk ids in increasing order, per parity f

@@ -268,7 +268,9 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ycoop=7), dict(ycoop=8, nt_loads=0), dict(ycoop=7, ycoop_ovh=64), dict(ycoop_ovh=0),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
-                dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1)]
+                dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
+                dict(fuse_plan=0, gen_split=1, gen_dense=1), dict(dense_g=4), dict(dense_g=32), dict(dense_g=128),
+                dict(count_grid=3), dict(count_grid=0, dense_g=16), dict(gen_dense=0), dict(gen_dense=1, dense_g=8)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

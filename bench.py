@@ -620,6 +620,19 @@ def main(argv=None):
                 ceil_tf = best * 64 / 1e12
                 alt[other]["roofline_valu"]["measured_ceiling"] = {
                     "TFLOPs": round(ceil_tf, 1), "frac": round(tf / ceil_tf, 4), "source": os.path.relpath(vp, ROOT)}
+                # The whole call's VALU issue (sweeps AND the overlapped RNG) against the same ceiling: the
+                # instruction count per call from a PMC pass (profiles/valu_issue.json), over this wall time.
+                vi = os.path.join(ROOT, "profiles", "valu_issue.json")
+                key = f"{name}/{other}"
+                if os.path.exists(vi) and key in json.load(open(vi)).get("per_call_valu_wave_instr", {}):
+                    n_instr = json.load(open(vi))["per_call_valu_wave_instr"][key]
+                    rate = n_instr / (ms2 * 1e-3)
+                    alt[other]["roofline_valu"]["call_issue"] = {
+                        "valu_wave_instr_per_call": n_instr, "achieved_per_s": round(rate, 1),
+                        "ceiling_per_s": best, "frac": round(rate / best, 4),
+                        "source": os.path.relpath(vi, ROOT),
+                        "note": "SQ_INSTS_VALU of every kernel of one call (sweeps + RNG) / wall ms_per_step, "
+                                "against tools/valu_probe's FP64 issue ceiling"}
         g.close()
 
     parity = None

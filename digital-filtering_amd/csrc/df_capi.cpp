@@ -103,6 +103,7 @@ struct df_handle {
     // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
+    int ablate_handoff = 0; // DFAMD_ABLATE_HANDOFF: timing-only ablation of the per-call stream hand-off
     int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
     // Dense generation (RngGeom::gen_dense: compaction through memory, one wave per needed 64-rank chunk,
     // near-1 log lanes deferred). Default in table mode (VALU-bound, where K3's skeleton costs); packed
@@ -387,7 +388,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
 {
     const int set = (int)(h->gen_launched & 1);
     rs = h->overlap ? h->rng_stream : h->stream;
-    HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
+    if (!(h->ablate_handoff & 2)) HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
@@ -503,11 +504,13 @@ int launch_gen(df_handle *h)
 // Start a visible step on the next generation (reference: generate_white_noise()).
 int consume_gen(df_handle *h)
 {
-    if (h->gen_used > 0) HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP); // previous set free
+    // DFAMD_ABLATE_HANDOFF (timing only, wrong results possible): 1 no wait for the noise, 2 no release
+    if (h->gen_used > 0 && !(h->ablate_handoff & 2))
+        HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP); // previous set free
     int rc;
     if (h->gen_launched == h->gen_used && (rc = launch_gen(h))) return rc;
     h->cur = (int)(h->gen_used & 1);
-    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[h->cur], 0), DF_EHIP);
+    if (!(h->ablate_handoff & 1)) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[h->cur], 0), DF_EHIP);
     h->gen_used++;
     return DF_OK;
 }
@@ -769,6 +772,7 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE || h->ycoop < 7 ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_FUSE_PLAN")) h->fuse_plan = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_ABLATE_HANDOFF")) h->ablate_handoff = std::atoi(e);
     h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
     const int Ny = s.Ny;

@@ -61,7 +61,7 @@ int fail(int code, const std::string &msg)
 
 struct CompDev {
     int Nyp = 0, Nzp = 0, rz_pitch = 0;
-    double *ry[2] = {}, *rz[2] = {}; // double-buffered noise: set k%2 feeds call k
+    double *ry[kMaxNoiseSets] = {}, *rz[kMaxNoiseSets] = {}; // noise set g % nsets feeds generation g
     double *By = nullptr, *Bz = nullptr;
     long long *byoff = nullptr, *bzoff = nullptr;
     int *Ny_st = nullptr, *Nz_st = nullptr;     // tap range per (strip, row), [s*Ny + j]
@@ -156,8 +156,15 @@ struct df_handle {
     hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
     hipEvent_t ev_halo = nullptr;            // split counting: the halo of the call just enqueued is done
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
-    long long gen_launched = 0; // generations enqueued (generation n reads state slot n%2, writes (n+1)%2)
+    long long gen_launched = 0; // generations enqueued (generation n reads state slot n%nsets, writes (n+1)%nsets)
     long long gen_used = 0;     // generations consumed by a visible step (ctor step 0, filter, stage API)
+    // Hand-off batch (round 3): the two cross-stream hand-offs of a call (noise ready -> sweeps; sweeps done
+    // -> noise set reusable) cost 5-15 us of queue packets per call on small planes (tools/handoff_ab.py,
+    // profiles/r3/h). With hb > 1 the generations go in epochs of hb calls over 2*hb noise sets: one
+    // noise-ready wait and one release record on the sweep stream per epoch instead of per call.
+    int hb = 1;
+    int nsets = 2;
+    long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
     RngGeom geom{};
     // halo
@@ -380,15 +387,25 @@ int drain_profile(df_handle *h)
 
 // ---------------------------------------------------------------- phases
 
+// Epochs of the noise pipeline: with hb == 1 every generation is its own epoch (absolute index, so the
+// event parity is the noise-set parity, as the graph path assumes); with hb > 1, epochs of hb
+// generations counted from gen_base.
+long long gen_epoch(const df_handle *h, long long g) { return h->hb == 1 ? g : (g - h->gen_base) / h->hb; }
+int gen_pos(const df_handle *h, long long g) { return h->hb == 1 ? 0 : (int)((g - h->gen_base) % h->hb); }
+int gen_set(const df_handle *h, long long g) { return (int)(g % h->nsets); }
+
 // Noise pipeline. The reference draws all six noise arrays at the start of each
 // call (df.cpp:453); the draws depend only on the stream state, so generation n+1
 // is enqueued on rng_stream as soon as call n's sweeps are enqueued, into the
 // other noise set, and runs (compute-bound) under call n's memory-bound sweeps.
 int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
 {
-    const int set = (int)(h->gen_launched & 1);
+    const long long gi = h->gen_launched, e = gen_epoch(h, gi);
+    const int set = gen_set(h, gi);
     rs = h->overlap ? h->rng_stream : h->stream;
-    if (!(h->ablate_handoff & 2)) HIP_OR(hipStreamWaitEvent(rs, h->ev_release[set], 0), DF_EHIP); // set no longer read
+    // the epoch's sets were last read by epoch e - 2 (2*hb sets), released when epoch e - 1 began
+    if (gen_pos(h, gi) == 0 && (h->hb == 1 || e >= 2) && !(h->ablate_handoff & 2))
+        HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e & 1], 0), DF_EHIP);
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
@@ -403,7 +420,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
         ev_record(h, 4);
         h->ev[h->ev_used].rng = true;
     }
-    const RngStateDev *in = h->rstate + (h->gen_launched & 1);
+    const RngStateDev *in = h->rstate + gen_set(h, gi);
     if (!h->split_count)
         HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs),
                DF_EHIP);
@@ -416,16 +433,17 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
 
 int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
-    const int set = (int)(h->gen_launched & 1);
+    const long long gi = h->gen_launched;
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
     // split counting exchanges counts only: K3 recomputes the accept flags of the waves it runs
     // (g.recount), a sixth or less of all waves on an interior rank of 8
-    HIP_OR(launch_rng_finish(g, h->rstate + (h->gen_launched & 1), h->rstate + ((h->gen_launched + 1) & 1),
-                             h->counts, h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks,
-                             h->err_dev, h->rng_blocks, nb_scan, rs),
+    HIP_OR(launch_rng_finish(g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->counts,
+                             h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks, h->err_dev,
+                             h->rng_blocks, nb_scan, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5);
-    HIP_OR(hipEventRecord(h->ev_rng[set], rs), DF_EHIP);
+    if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
+        HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
     h->gen_launched++;
     return DF_OK;
 }
@@ -504,20 +522,31 @@ int launch_gen(df_handle *h)
 // Start a visible step on the next generation (reference: generate_white_noise()).
 int consume_gen(df_handle *h)
 {
-    // DFAMD_ABLATE_HANDOFF (timing only, wrong results possible): 1 no wait for the noise, 2 no release
-    if (h->gen_used > 0 && !(h->ablate_handoff & 2))
-        HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP); // previous set free
+    const long long gi = h->gen_used, e = gen_epoch(h, gi);
+    const bool first = gen_pos(h, gi) == 0;
     int rc;
-    if (h->gen_launched == h->gen_used && (rc = launch_gen(h))) return rc;
-    h->cur = (int)(h->gen_used & 1);
-    if (!(h->ablate_handoff & 1)) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[h->cur], 0), DF_EHIP);
+    // DFAMD_ABLATE_HANDOFF (timing only, wrong results possible): 1 no wait for the noise, 2 no release
+    if (first && gi > (h->hb == 1 ? 0 : h->gen_base) && !(h->ablate_handoff & 2))
+        HIP_OR(hipEventRecord(h->ev_release[(e - 1) & 1], h->stream), DF_EHIP); // the previous epoch's sets free
+    const long long need = h->hb == 1 ? gi + 1 : h->gen_base + (e + 1) * h->hb; // this epoch, launched
+    while (h->gen_launched < need)
+        if ((rc = launch_gen(h))) return rc;
+    if (first && !(h->ablate_handoff & 1)) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[e & 1], 0), DF_EHIP);
+    h->cur = gen_set(h, gi);
     h->gen_used++;
     return DF_OK;
 }
 
+// After a visible step's sweeps are enqueued: the next epoch's generations, under those sweeps.
 int prefetch_gen(df_handle *h)
 {
-    if (h->overlap && h->gen_launched == h->gen_used) return launch_gen(h);
+    if (!h->overlap || h->gen_used == 0) return DF_OK;
+    const long long gi = h->gen_used - 1; // the generation this step consumed
+    if (gen_pos(h, gi) != 0) return DF_OK;
+    const long long need = h->hb == 1 ? h->gen_used + 1 : h->gen_base + (gen_epoch(h, gi) + 2) * h->hb;
+    int rc;
+    while (h->gen_launched < need)
+        if ((rc = launch_gen(h))) return rc;
     return DF_OK;
 }
 
@@ -988,7 +1017,7 @@ int alloc_components(df_handle *h)
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
         const ComponentSetup &F = s.comp[c];
-        for (int set = 0; set < 2; ++set) {
+        for (int set = 0; set < h->nsets; ++set) {
             if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp) * h->Pz))) return rc;
             if ((rc = dalloc_t(h, &d.rz[set], (size_t)Ny * d.rz_pitch))) return rc;
         }
@@ -1085,7 +1114,7 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         g.Nzp[c] = h->c[c].Nzp;
         g.rz_pitch[c] = h->c[c].rz_pitch;
     }
-    if ((rc = dalloc_t(h, &h->rstate, 2))) return rc;
+    if ((rc = dalloc_t(h, &h->rstate, h->nsets))) return rc;
     h->rng_chunk = (h->rng_blocks + h->world - 1) / h->world;
     const int nb_pad = h->rng_chunk * h->world;
     if ((rc = dalloc_t(h, &h->counts, nb_pad))) return rc;
@@ -1222,6 +1251,15 @@ int build(df_handle *h, const df_config_c *cfg)
     if (!build_setup(h->flow, h->spec, h->setup, err)) return fail(DF_EIO, err);
     if ((rc = plan_strips(h))) return rc;
     if ((rc = plan_rng(h))) return rc;
+    // Hand-off batch: small single-GPU planes, where the two per-call cross-stream hand-offs are 10-40% of
+    // a call (c2 packed -17%, the reference's grid -9%, c1 -40% with both removed; profiles/r3/h), take
+    // epochs of 4 calls over 8 noise sets (a few MB each there). Split planes and RCCL handles keep one
+    // hand-off per call (their RNG exchanges stay in call order with the halo).
+    if (h->world == 1 && !cfg->comm_id && (long long)h->Ny * h->Nz_loc <= (1ll << 20)) h->hb = 4;
+    if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
+    if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
+    if (h->world > 1 || cfg->comm_id) h->hb = 1;
+    h->nsets = h->hb > 1 ? 2 * h->hb : 2;
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -1294,9 +1332,8 @@ void drop_graphs(df_handle *h)
 // enqueued, no per-call events (profiling), no CSV, no RCCL.
 bool graph_ok(df_handle *h)
 {
-    return h->use_graph && h->overlap && h->world == 1 && !h->group && !h->profiling && !h->halo_loopback &&
-           h->csv_path.empty() &&
-           h->gen_launched == h->gen_used + 1;
+    return h->use_graph && h->hb == 1 && h->nsets == 2 && h->overlap && h->world == 1 && !h->group && !h->profiling &&
+           !h->halo_loopback && h->csv_path.empty() && h->gen_launched == h->gen_used + 1;
 }
 
 // Capture one call for noise set `cur`: sweeps on stream, the next generation (into set cur^1,
@@ -1806,13 +1843,28 @@ int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
     if (rc) return rc;
     RngStateDev st; // state after the last visible step: slot gen_used % 2 (a prefetched
                     // generation writes the other slot)
-    HIP_OR(hipMemcpyAsync(&st, h->rstate + (h->gen_used & 1), sizeof st, hipMemcpyDeviceToHost, h->stream),
+    HIP_OR(hipMemcpyAsync(&st, h->rstate + gen_set(h, h->gen_used), sizeof st, hipMemcpyDeviceToHost, h->stream),
            DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     if (state) *state = st.state;
     if (saved_flag) *saved_flag = st.saved_flag;
     if (saved) *saved = st.saved;
     return check_rng_error(h);
+}
+
+// Discard the prefetched generations (the caller has synchronized both streams) and start epoch 0 at
+// the next visible step with hand-off batch hb_new; with overlap its generations are enqueued now.
+static int restart_pipeline(df_handle *h, int hb_new)
+{
+    h->gen_launched = h->gen_used;
+    h->gen_base = h->gen_used;
+    h->hb = hb_new;
+    if (!h->overlap) return DF_OK;
+    const long long need = h->gen_used + h->hb;
+    int rc;
+    while (h->gen_launched < need)
+        if ((rc = launch_gen(h))) return rc;
+    return DF_OK;
 }
 
 int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
@@ -1823,12 +1875,11 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
     int rc = sync_all(h);
     if (rc) return rc;
     RngStateDev st{state, saved_flag ? 1 : 0, 0, saved};
-    HIP_OR(hipMemcpyAsync(h->rstate + (h->gen_used & 1), &st, sizeof st, hipMemcpyHostToDevice, h->stream), DF_EHIP);
+    HIP_OR(hipMemcpyAsync(h->rstate + gen_set(h, h->gen_used), &st, sizeof st, hipMemcpyHostToDevice, h->stream),
+           DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
-    if (h->gen_launched > h->gen_used) { // the prefetched noise came from the old state: redo it
-        h->gen_launched = h->gen_used;
-        if ((rc = launch_gen(h))) return rc;
-    }
+    if (h->gen_launched > h->gen_used) // the prefetched noise came from the old state: redo it
+        return restart_pipeline(h, h->hb);
     return DF_OK;
 }
 
@@ -1882,6 +1933,20 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
+    else if (k == "handoff_batch") {
+        if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
+        if (value > 1 && 2 * value > h->nsets)
+            return fail(DF_EINVAL, "handoff_batch " + std::to_string(value) + " needs " + std::to_string(2 * value) +
+                                       " noise sets; this handle has " + std::to_string(h->nsets) +
+                                       " (DFAMD_HANDOFF_BATCH at create)");
+        if (value > 1 && (h->world > 1 || h->comm || h->group))
+            return fail(DF_EINVAL, "handoff_batch > 1 is for single-GPU handles");
+        if (h->device >= 0 && value != h->hb) {
+            int rc = sync_all(h);
+            if (rc) return rc;
+            if ((rc = restart_pipeline(h, value))) return rc;
+        } else h->hb = value;
+    }
     else if (k == "count_grid") {
         if (value < 0) return fail(DF_EINVAL, "count_grid must be >= 0");
         h->geom.count_grid = value;

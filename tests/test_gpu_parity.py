@@ -270,7 +270,9 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(fuse_plan=0, gen_split=1, gen_dense=1), dict(dense_g=4), dict(dense_g=32), dict(dense_g=128),
-                dict(count_grid=3), dict(count_grid=0, dense_g=16), dict(gen_dense=0), dict(gen_dense=1, dense_g=8)]
+                dict(count_grid=3), dict(count_grid=0, dense_g=16), dict(gen_dense=0), dict(gen_dense=1, dense_g=8),
+                dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4), dict(handoff_batch=2, graph=1),
+                dict(handoff_batch=1, graph=1), dict(graph=0, handoff_batch=4)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -285,6 +287,27 @@ def test_runtime_tuning_is_bitexact(mode):
         b.set_tuning("rows_per_wave", 3)
     with pytest.raises(dfamd.DFError, match="power of two"):
         b.set_tuning("zwin_T", 3000)
+    with pytest.raises(dfamd.DFError, match="handoff_batch"):
+        b.set_tuning("handoff_batch", 3)
+
+
+@pytest.mark.parametrize("hb", ["1", "2", "4"])
+def test_handoff_batch_mid_epoch_state_changes(monkeypatch, hb):
+    # epochs of hb calls over 2*hb noise sets: a stream state set mid-epoch, the stage API and filter calls
+    # interleaved, checked against the oracle after every step
+    monkeypatch.setenv("DFAMD_HANDOFF_BATCH", hb)
+    spec = (48, 96, 2, 10)
+    o = oracle_synth(*spec, seed=13)
+    g = gpu_synth(*spec, seed=13)
+    for i in range(7):
+        o.filter(1e-8)
+        g.filter(1e-8)
+        if i == 2:  # mid-epoch: restart the pipeline from the oracle's current state
+            st = o.rng.state
+            g.set_rng_state(*st)
+        assert g.rng_state() == o.rng.state, i
+        for k in FIELDS:
+            assert np.array_equal(g.field(k), o.field(k)), (i, k)
 
 
 @pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90)])

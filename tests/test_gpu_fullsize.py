@@ -1,7 +1,8 @@
 """Full-size parity (BASELINE configs): c3 = 2048 x 2048, N 4-64 on one GPU.
 
-The oracle cannot hold c3's 20 GB of coefficients, so these tests restate the
-path for SAMPLED ROWS at full size: the oracle's RNG (pinned to the reference)
+c3's whole plane is compared with the oracle's whole plane (test_c3_whole_plane_bitexact_vs_oracle:
+20 GB of host coefficients, the OpenMP oracle, ~40 s). For the rest (c3 over more calls, c4, c5) the
+tests restate the path for SAMPLED ROWS at full size: the oracle's RNG (pinned to the reference)
 regenerates the whole call's stream (2.7e7 normals), numpy applies the y-pass,
 z-pass, correlation, RST and SRA to the sampled rows in the reference's order
 (df.cpp:359-481), and the GPU fields must agree there to 1e-6 (observed ~1e-15).
@@ -281,3 +282,50 @@ def test_create_destroy_releases_device_memory():
         g.close()
     after = free_bytes()
     assert before - after < 64 << 20, (before, after)  # allocator slack only, not ~0.7 GB per handle
+
+
+ORACLE_C3_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import oracle as O
+o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=2048, Nz=2048, N_min=4, N_max=64, seed=int(sys.argv[3]))
+out = {"s0_" + k: v for k, v in o.fields().items()}
+s0 = o.rng.state
+o.filter(1e-8)
+out.update({"s1_" + k: v for k, v in o.fields().items()})
+s1 = o.rng.state
+np.savez(sys.argv[2], state0=np.array([s0[0], s0[1]], dtype=np.uint64), saved0=s0[2],
+         state1=np.array([s1[0], s1[1]], dtype=np.uint64), saved1=s1[2], **out)
+"""
+
+
+def test_c3_whole_plane_bitexact_vs_oracle(tmp_path):
+    """c3 (BASELINE configs[2], 2048 x 2048, N 4-64): the WHOLE plane, step 0 and one filter(1e-8), against
+    the oracle's whole plane (oracle/df_oracle.c with OpenMP over the sweep rows, 20 GB of host
+    coefficients, ~40 s on 16 cores), in both coefficient modes: every field bit for bit, and the stream
+    state (the full sizes were checked on sampled rows only)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "oracle", "liboracle_omp.so")
+    if not os.path.exists(lib):
+        pytest.skip("oracle/liboracle_omp.so not built")
+    npz = str(tmp_path / "c3_oracle.npz")
+    env = dict(os.environ, ORACLE_LIB=lib, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "16"))
+    r = subprocess.run([sys.executable, "-c", ORACLE_C3_SCRIPT, os.path.join(root, "oracle"), npz, "77"], env=env,
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ref = np.load(npz)
+    for mode in ("table", "packed"):
+        g = dfamd.DigitalFilter(plane="synthetic", seed=77, device=0, coeff_mode=mode, **C3)
+        st = g.rng_state()
+        assert (st[0], st[1], st[2]) == (int(ref["state0"][0]), int(ref["state0"][1]), float(ref["saved0"])), mode
+        for k in ("u", "v", "w"):  # step 0: no correlation, no SRA (df.cpp:57-62)
+            assert np.array_equal(g.field(k), ref["s0_" + k]), (mode, "step0", k)
+        g.filter(1e-8)
+        st = g.rng_state()
+        assert (st[0], st[1], st[2]) == (int(ref["state1"][0]), int(ref["state1"][1]), float(ref["saved1"])), mode
+        for k in ("u", "v", "w", "T", "rho"):
+            assert np.array_equal(g.field(k), ref["s1_" + k]), (mode, "step1", k)
+        g.close()

@@ -880,33 +880,28 @@ __global__ __launch_bounds__(kRngThreads) void rng_dense_generate_kernel(RngGeom
         const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
         const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
         const long long rank = c * 64 + lane;
+        const uint64_t q = f + 2ull * (uint64_t)rank;
         const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform
-        // the chunk's 128 positions: array, row base and stored column ranges once per chunk (scalar), so a
-        // lane's destination is a few 32-bit compares and adds with no per-lane 64-bit row multiply
-        const WaveDest wd = wave_dest(g, q0, 128);
+        const StreamPos P0 = stream_pos(g, q0);
+        const int su = P0.sidx < 6 ? P0.sidx : 5;
+        const uint32_t W = g.width[su];
+        const bool generic = P0.sidx >= 6 || W < 128 || q0 + 128 > g.seg[su + 1];
         double *d0 = nullptr, *d1 = nullptr;
         const bool live = rank < A;
         if (live) {
-            if (!wd.generic) { // one array, at most one row wrap (rows >= 128 normals)
-                uint32_t col = wd.col + 2u * (uint32_t)lane;
-                double *rp = wd.base + (size_t)wd.row * wd.pitch;
-                if (col >= wd.W) {
-                    col -= wd.W;
-                    rp += wd.pitch;
+            if (!generic) { // one array, at most one row wrap
+                uint32_t row = P0.row, col = P0.col + 2u * (uint32_t)lane;
+                if (col >= W) {
+                    col -= W;
+                    ++row;
                 }
-                auto dest = [&](double *rowp, uint32_t cc) -> double * {
-                    if (cc >= wd.lo1 && cc < wd.hi1) return rowp + ((int)cc + wd.o1);
-                    if (cc >= wd.lo2) return rowp + ((int)cc + wd.o2);
-                    return nullptr;
-                };
-                d0 = dest(rp, col);
-                if (++col == wd.W) {
+                d0 = stream_dest(g, StreamPos{su, row, col});
+                if (++col == W) {
                     col = 0;
-                    rp += wd.pitch;
+                    ++row;
                 }
-                d1 = dest(rp, col); // q + 1 < the array's end
+                d1 = stream_dest(g, StreamPos{su, row, col}); // q + 1 < the array's end
             } else {
-                const uint64_t q = f + 2ull * (uint64_t)rank;
                 const StreamPos p0 = stream_pos(g, q);
                 d0 = stream_dest(g, p0);
                 d1 = (q + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;

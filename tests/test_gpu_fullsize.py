@@ -284,12 +284,14 @@ def test_create_destroy_releases_device_memory():
     assert before - after < 64 << 20, (before, after)  # allocator slack only, not ~0.7 GB per handle
 
 
-ORACLE_C3_SCRIPT = r"""
+ORACLE_PLANE_SCRIPT = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1])
 import oracle as O
-o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=2048, Nz=2048, N_min=4, N_max=64, seed=int(sys.argv[3]))
-out = {"s0_" + k: v for k, v in o.fields().items()}
+Ny, Nz = int(sys.argv[4]), int(sys.argv[5])
+o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=Ny, Nz=Nz, N_min=4, N_max=64, seed=int(sys.argv[3]))
+print("oracle step 0 done", flush=True)
+out = {"s0_" + k: v for k, v in o.fields().items() if k in ("u", "v", "w")}
 s0 = o.rng.state
 o.filter(1e-8)
 out.update({"s1_" + k: v for k, v in o.fields().items()})
@@ -299,11 +301,9 @@ np.savez(sys.argv[2], state0=np.array([s0[0], s0[1]], dtype=np.uint64), saved0=s
 """
 
 
-def test_c3_whole_plane_bitexact_vs_oracle(tmp_path):
-    """c3 (BASELINE configs[2], 2048 x 2048, N 4-64): the WHOLE plane, step 0 and one filter(1e-8), against
-    the oracle's whole plane (oracle/df_oracle.c with OpenMP over the sweep rows, 20 GB of host
-    coefficients, ~40 s on 16 cores), in both coefficient modes: every field bit for bit, and the stream
-    state (the full sizes were checked on sampled rows only)."""
+def oracle_whole_plane(tmp_path, Ny, Nz, seed):
+    """The oracle (oracle/df_oracle.c, OpenMP over the sweep rows) on a whole BASELINE plane: step 0 and
+    one filter(1e-8); 20 GB (c3) to 85 GB (c4, c5) of host coefficients."""
     import os
     import subprocess
     import sys
@@ -311,21 +311,51 @@ def test_c3_whole_plane_bitexact_vs_oracle(tmp_path):
     lib = os.path.join(root, "oracle", "liboracle_omp.so")
     if not os.path.exists(lib):
         pytest.skip("oracle/liboracle_omp.so not built")
-    npz = str(tmp_path / "c3_oracle.npz")
+    npz = str(tmp_path / f"oracle_{Ny}x{Nz}.npz")
     env = dict(os.environ, ORACLE_LIB=lib, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "16"))
-    r = subprocess.run([sys.executable, "-c", ORACLE_C3_SCRIPT, os.path.join(root, "oracle"), npz, "77"], env=env,
-                       capture_output=True, text=True, timeout=280)
+    r = subprocess.run([sys.executable, "-c", ORACLE_PLANE_SCRIPT, os.path.join(root, "oracle"), npz, str(seed),
+                        str(Ny), str(Nz)], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
-    ref = np.load(npz)
+    return np.load(npz)
+
+
+def check_against_oracle(handles, ref, what):
+    """handles: one whole-plane handle or the z-strips of one plane, right after construction."""
+    def state_ok(key, saved):
+        return all(h.rng_state() == (int(ref[key][0]), int(ref[key][1]), float(ref[saved])) for h in handles)
+
+    def cat(k):
+        return np.concatenate([h.field(k) for h in handles], axis=1)
+    assert state_ok("state0", "saved0"), what
+    for k in ("u", "v", "w"):  # step 0: no correlation, no SRA (df.cpp:57-62)
+        assert np.array_equal(cat(k), ref["s0_" + k]), (what, "step0", k)
+    if len(handles) == 1:
+        handles[0].filter(1e-8)
+    else:
+        dfamd.filter_group(handles, 1e-8)
+    assert state_ok("state1", "saved1"), what
+    for k in ("u", "v", "w", "T", "rho"):
+        assert np.array_equal(cat(k), ref["s1_" + k]), (what, "step1", k)
+    for h in handles:
+        h.close()
+
+
+def test_c3_whole_plane_bitexact_vs_oracle(tmp_path):
+    """c3 (BASELINE configs[2], 2048 x 2048, N 4-64): the WHOLE plane against the oracle's whole plane, in
+    both coefficient modes: every field bit for bit, and the stream state (the full sizes
+    were checked on sampled rows only)."""
+    ref = oracle_whole_plane(tmp_path, 2048, 2048, 77)
     for mode in ("table", "packed"):
-        g = dfamd.DigitalFilter(plane="synthetic", seed=77, device=0, coeff_mode=mode, **C3)
-        st = g.rng_state()
-        assert (st[0], st[1], st[2]) == (int(ref["state0"][0]), int(ref["state0"][1]), float(ref["saved0"])), mode
-        for k in ("u", "v", "w"):  # step 0: no correlation, no SRA (df.cpp:57-62)
-            assert np.array_equal(g.field(k), ref["s0_" + k]), (mode, "step0", k)
-        g.filter(1e-8)
-        st = g.rng_state()
-        assert (st[0], st[1], st[2]) == (int(ref["state1"][0]), int(ref["state1"][1]), float(ref["saved1"])), mode
-        for k in ("u", "v", "w", "T", "rho"):
-            assert np.array_equal(g.field(k), ref["s1_" + k]), (mode, "step1", k)
-        g.close()
+        check_against_oracle([dfamd.DigitalFilter(plane="synthetic", seed=77, device=0, coeff_mode=mode, **C3)],
+                             ref, mode)
+
+
+@pytest.mark.parametrize("name,Ny,Nz", [("c4", 2048, 8192), ("c5", 4096, 4096)])
+def test_multi_gpu_planes_whole_bitexact_vs_oracle(tmp_path, name, Ny, Nz):
+    """BASELINE configs[3] (c4) and configs[4] (c5), the multi-GPU planes: the whole plane in table mode
+    and its 8-way z-strip split in packed mode (the partition bench.py --gpus 8 runs; 85 GB of coefficients
+    between the strips, in-process halo copies) against the oracle's whole plane, bit for bit."""
+    ref = oracle_whole_plane(tmp_path, Ny, Nz, 78)
+    spec = dict(plane="synthetic", seed=78, device=0, Ny=Ny, Nz=Nz, N_min=4, N_max=64)
+    check_against_oracle([dfamd.DigitalFilter(coeff_mode="table", **spec)], ref, name + " table")
+    check_against_oracle(dfamd.create_group(8, coeff_mode="packed", **spec), ref, name + " packed x8 strips")

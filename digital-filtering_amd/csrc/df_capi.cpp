@@ -163,6 +163,7 @@ struct df_handle {
     // profiles/r3/h). With hb > 1 the generations go in epochs of hb calls over 2*hb noise sets: one
     // noise-ready wait and one release record on the sweep stream per epoch instead of per call.
     int hb = 1;
+    int hb_burst = 0; // 1: an epoch's generations enqueued in one burst (measured against spread, profiles/r3/m)
     int nsets = 2;
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
@@ -537,13 +538,19 @@ int consume_gen(df_handle *h)
     return DF_OK;
 }
 
-// After a visible step's sweeps are enqueued: the next epoch's generations, under those sweeps.
+// After a visible step's sweeps are enqueued: generations up to hb steps ahead, under those sweeps.
+// hb_burst 1 enqueues a whole epoch at its predecessor's first step instead (one burst of hb
+// generations); spread (the default) enqueues one per step, so the last generation of epoch e + 1 goes
+// under the last step of epoch e, just before epoch e + 1 waits for it.
 int prefetch_gen(df_handle *h)
 {
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
-    if (gen_pos(h, gi) != 0) return DF_OK;
-    const long long need = h->hb == 1 ? h->gen_used + 1 : h->gen_base + (gen_epoch(h, gi) + 2) * h->hb;
+    long long need = h->gen_used + h->hb;
+    if (h->hb_burst && h->hb > 1) {
+        if (gen_pos(h, gi) != 0) return DF_OK;
+        need = h->gen_base + (gen_epoch(h, gi) + 2) * h->hb;
+    }
     int rc;
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
@@ -1265,6 +1272,7 @@ int build(df_handle *h, const df_config_c *cfg)
         if (h->world == 1 && !cfg->comm_id && nymax < 128) h->hb = cells <= (1ll << 16) ? 4 : cells <= (1ll << 20) ? 2 : 1;
     }
     if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_HB_BURST")) h->hb_burst = std::atoi(e);
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;

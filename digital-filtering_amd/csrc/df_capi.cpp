@@ -70,6 +70,7 @@ struct CompDev {
     long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
     long long by_size = 0, bz_size = 0;   // reference offset-packed sizes (this strip's cells)
     int ycoop2_xcd[9] = {};               // row-pair y-pass tiles of XCD x: [ycoop2_xcd[x], ycoop2_xcd[x+1])
+    int *ycoop2_perm = nullptr;           // row-pair y-pass: dispatch position -> tile (within each XCD run)
     double sa = 0, s1a = 0;
 };
 
@@ -117,7 +118,11 @@ struct df_handle {
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
+    int ycoop_map = 0;   // row-pair y-pass tiles to XCDs: 0 equal-byte contiguous runs, 1 interleaved (t % 8)
+    int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
+                         // consecutive tiles, heaviest group first (balance_ycoop2)
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
+    std::vector<int> ycoop2_perm_host[3]; // balance_ycoop2's dispatch order (uploaded to CompDev::ycoop2_perm)
     // z-strips: 1 = every rank counts every attempt block, so the halo send/recv is the call's only
     // collective (SURVEY 8e option B, north star "single RCCL halo exchange"; the packed default).
     // 0 = split counting plus a per-call all-gather of block and wave counts (option A), ordered after
@@ -309,7 +314,11 @@ SweepArgs sweep_args(df_handle *h)
             a.ycoop2_xcd[c][x] = h->c[c].ycoop2_xcd[x];
             a.ycoop2_run = std::max(a.ycoop2_run, h->c[c].ycoop2_xcd[x + 1] - h->c[c].ycoop2_xcd[x]);
         }
-    for (int c = 0; c < 3; ++c) a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
+    for (int c = 0; c < 3; ++c) {
+        a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
+        a.ycoop2_perm[c] = h->ycoop_order ? h->c[c].ycoop2_perm : nullptr;
+    }
+    a.ycoop2_map = h->ycoop_map;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -757,6 +766,34 @@ void balance_ycoop2(df_handle *h, int c)
         while (x < 8 && acc >= tot * x / 8) xr[x++] = (int)t + 1;
     }
     while (x <= 8) xr[x++] = (int)wgt.size();
+    // Dispatch order inside each XCD run. Ascending rows (order 0) keeps neighbouring row pairs, which share
+    // most noise rows, resident together; but where the widest stencils sit at the end of a run (the
+    // reference's grid: N_y peaks at 212 around j = 170, N 28-60 elsewhere) they start last and the run
+    // ends on a tail of 27-chunk blocks. Order g >= 1: groups of g consecutive tiles, heaviest group first.
+    h->ycoop2_perm_host[c].assign(wgt.size(), 0);
+    std::vector<int> &perm = h->ycoop2_perm_host[c];
+    for (size_t t = 0; t < perm.size(); ++t) perm[t] = (int)t;
+    const int gsz = h->ycoop_order;
+    if (gsz > 0)
+        for (int xx = 0; xx < 8; ++xx) {
+            std::vector<std::pair<double, int>> grp; // (group weight, first tile)
+            for (int t = xr[xx]; t < xr[xx + 1]; t += gsz) {
+                double w = 0;
+                for (int u = t; u < std::min(t + gsz, xr[xx + 1]); ++u) w += wgt[u];
+                grp.push_back({w, t});
+            }
+            std::stable_sort(grp.begin(), grp.end(), [](const auto &p, const auto &q) { return p.first > q.first; });
+            int pos = xr[xx];
+            for (const auto &gq : grp)
+                for (int u = gq.second; u < std::min(gq.second + gsz, xr[xx + 1]); ++u) perm[pos++] = u;
+        }
+}
+
+// Upload the dispatch order of the row-pair y-pass (alloc_components, df_set_tuning).
+int upload_ycoop2_perm(df_handle *h, int c)
+{
+    if (!h->c[c].ycoop2_perm || h->ycoop2_perm_host[c].empty()) return DF_OK;
+    return upload(h, h->c[c].ycoop2_perm, h->ycoop2_perm_host[c].data(), h->ycoop2_perm_host[c].size());
 }
 
 // This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
@@ -793,7 +830,13 @@ int plan_strips(df_handle *h)
         // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
         // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
         // c3-class planes lose with it.
-        if (h->coeff_mode == DF_COEFF_PACKED && long_chain) h->ycoop = 7;
+        // Inside each XCD run, groups of 4 tiles go heaviest first (ycoop_order 4): the widest stencils no
+        // longer start last (reference's grid y-pass -2.5%; ascending order 0 and groups of 1/16/64 measured
+        // alongside in profiles/r3/p).
+        if (h->coeff_mode == DF_COEFF_PACKED && long_chain) {
+            h->ycoop = 7;
+            h->ycoop_order = 4;
+        }
         // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
         // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
         // profiles/r2/ab_zsplit.jsonl)
@@ -1046,7 +1089,9 @@ int alloc_components(df_handle *h)
                 }
         }
         h->y_nst[c] = Nst[0]; // host copy for the row-block y-pass's XCD balance
+        if ((rc = dalloc_t(h, &d.ycoop2_perm, (size_t)h->nstrips * ((Ny + 1) / 2)))) return rc;
         balance_ycoop2(h, c);
+        if ((rc = upload_ycoop2_perm(h, c))) return rc;
         if ((rc = dalloc_t(h, &d.Ny_st, Nst[0].size()))) return rc;
         if ((rc = dalloc_t(h, &d.Nz_st, Nst[1].size()))) return rc;
         if ((rc = upload(h, d.Ny_st, Nst[0].data(), Nst[0].size()))) return rc;
@@ -1913,7 +1958,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->rows_per_wave = value;
     } else if (k == "nt_loads") h->nt_loads = value != 0;
     else if (k == "heavy_first") h->heavy_first = value != 0;
-    else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
+    else if (k == "yunroll") h->yunroll = value >= 32 ? 32 : value >= 16 ? 16 : value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = h->ynt_stores = value != 0;
     else if (k == "znt_stores") h->nt_stores = value != 0;
@@ -1925,7 +1970,28 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ycoop_ovh") {
         if (value < 0) return fail(DF_EINVAL, "ycoop_ovh must be >= 0");
         h->ycoop_ovh = value;
-        for (int c = 0; c < 3; ++c) balance_ycoop2(h, c);
+        if (valid_dev(h)) {
+            if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
+            for (int c = 0; c < 3; ++c) {
+                balance_ycoop2(h, c);
+                if (int rc = upload_ycoop2_perm(h, c)) return rc;
+            }
+        }
+    }
+    else if (k == "ycoop_map") {
+        if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");
+        h->ycoop_map = value;
+    }
+    else if (k == "ycoop_order") {
+        if (value < 0) return fail(DF_EINVAL, "ycoop_order must be >= 0");
+        h->ycoop_order = value;
+        if (valid_dev(h)) {
+            if (int rc = sync_all(h)) return rc;
+            for (int c = 0; c < 3; ++c) {
+                balance_ycoop2(h, c);
+                if (int rc = upload_ycoop2_perm(h, c)) return rc;
+            }
+        }
     }
     else if (k == "ycoop") {
         if (value < 0 || value > 8 || value == 5 || value == 6)

@@ -1519,8 +1519,21 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int Ny = a.Ny, nrowblk = (Ny + RR - 1) / RR;
     const int x = blockIdx.x & 7;
-    const int tile = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
-    if (tile >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
+    int pos;
+    if (a.ycoop2_map == 1) { // interleaved: tile t on XCD t % 8, no empty blocks
+        pos = (int)blockIdx.x;
+        if (pos >= a.nstrips * nrowblk) return;
+    } else {
+        pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
+        if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
+    }
+#if defined(DF_COOP2_ONLY_XCD)
+    if (x != DF_COOP2_ONLY_XCD) return; // timing only: one XCD's run alone
+#endif
+#if defined(DF_COOP2_SKIP_XCD)
+    if (x == DF_COOP2_SKIP_XCD) return; // timing only: every run but one XCD's
+#endif
+    const int tile = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos;
     const int s = tile / nrowblk;             // rows ascending within a strip (L2 reuse of noise rows)
     const int j0 = (tile - s * nrowblk) * RR;
     const int nr = min(RR, Ny - j0);
@@ -1586,9 +1599,37 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
 #pragma unroll
             for (int i = 0; i < RH; ++i) {
                 // this chunk's noise rows of row 2i + rs: u in [ua, ub) (wave-uniform)
-                const int ua = max(0, lor[i] - mlo - u0), ub = min(CHG, hir[i] - mlo - u0 + 1);
+                const int ua = __builtin_amdgcn_readfirstlane(max(0, lor[i] - mlo - u0));
+                const int ub = __builtin_amdgcn_readfirstlane(min(CHG, hir[i] - mlo - u0 + 1));
                 const double *pc = reinterpret_cast<const double *>(prod + (2 * i + rs) * CH * 64) + cell;
-                for (int u = ua; u < ub; ++u) acc[i] += pc[u * 2 * P];
+#if defined(DF_COOP2_SERIAL_SUM)
+                for (int u = ua; u < ub; ++u) acc[i] += pc[u * 2 * P]; // timing only: one LDS round trip per add
+#elif defined(DF_ABLATE_COOPSUM)
+                if (ua < ub) acc[i] += pc[ua * 2 * P]; // timing only: one product per chunk
+#else
+                // LDS reads issued 8 at a time, then their adds in tap order: one add per LDS round trip made
+                // the sum a serial chain of LDS latencies (CHG = 128 of them per chunk on a folded narrow strip).
+                if (P == 64 && ua == 0 && ub == CHG) { // whole chunk of a full strip: immediate offsets
+#pragma unroll
+                    for (int g = 0; g < CH; g += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] = pc[(g + e) * 128];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) acc[i] += v[e];
+                    }
+                } else {
+                    // slots past ub (clamped into the chunk) are read but never added: the same additions
+                    for (int g = ua; g < ub; g += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) v[e] = pc[min(g + e, CHG - 1) * 2 * P];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e)
+                            if (g + e < ub) acc[i] += v[e]; // wave-uniform condition
+                    }
+                }
+#endif
             }
         }
         __syncthreads();
@@ -1614,6 +1655,16 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     if (TABLE && a.per_cell)
         hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
     else if (!TABLE && a.nt_loads) {
+        if constexpr (R <= 2) { // deeper rings (16 or 32 taps in flight) for one or two rows per wave
+            if (a.yunroll >= 32) {
+                hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 32, false>), grid, dim3(256), 0, st, a, nrowblk);
+                return hipGetLastError();
+            }
+            if (a.yunroll >= 16) {
+                hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 16, false>), grid, dim3(256), 0, st, a, nrowblk);
+                return hipGetLastError();
+            }
+        }
         if (a.yunroll >= 8)
             hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
         else if (a.yunroll >= 4)
@@ -1634,7 +1685,8 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
     if (!table && a.ycoop >= 7) { // row pairs: 7 = 4 noise rows per wave per chunk (32 KiB LDS), 8 = 8 (64 KiB)
-        const dim3 grid((unsigned)(8 * a.ycoop2_run), 3);
+        const unsigned tiles = (unsigned)(a.nstrips * ((a.Ny + 1) / 2));
+        const dim3 grid(a.ycoop2_map == 1 ? (tiles + 7) / 8 * 8 : (unsigned)(8 * a.ycoop2_run), 3);
         if (a.ycoop == 7) {
             if (a.nt_loads) hipLaunchKernelGGL((ypass_coop2_kernel<true, 4>), grid, dim3(256), 0, st, a);
             else hipLaunchKernelGGL((ypass_coop2_kernel<false, 4>), grid, dim3(256), 0, st, a);

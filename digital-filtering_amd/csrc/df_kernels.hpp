@@ -119,6 +119,8 @@ struct SweepArgs {
     int ycoop;              // packed y-pass: one block per (strip, row) tile, taps shared by 4 waves (long chains)
     int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)
     int ycoop2_run;         // the longest such run (grid = 8 x this)
+    const int *ycoop2_perm[3]; // dispatch position -> tile inside each run (nullptr: ascending)
+    int ycoop2_map;            // 0: XCD x runs tiles [ycoop2_xcd[c][x], ...); 1: tile t on XCD t % 8 (interleaved)
     int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
     int ydeep;              // table y-pass: noise and coefficients loaded a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)

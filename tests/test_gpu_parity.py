@@ -162,6 +162,26 @@ def test_golden_native_grid(mode, tuning):
             assert np.allclose(st3, g[f"s{s}_{k}_stats"], rtol=1e-9, atol=1e-300), (s, k)
 
 
+@pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=8)), ("packed", dict(ycoop_order=1)),
+                                         ("packed", dict(ycoop_order=8)), ("packed", dict(ycoop_map=1)),
+                                         ("table", {})])
+def test_native_grid_bitexact_vs_oracle(mode, tuning):
+    # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
+    # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
+    o = O.Filter(plane=O.PLANE_NATIVE, seed=42)
+    g = dfamd.DigitalFilter(seed=42, device=0, coeff_mode=mode)
+    for k, v in tuning.items():
+        g.set_tuning(k, v)
+    for dt in (None, 1e-8, 1e-5):
+        if dt is not None:
+            o.filter(dt)
+            g.filter(dt)
+        gf, of = g.fields(), o.fields()
+        for k in FIELDS:
+            assert np.array_equal(gf[k], of[k]), (dt, k, float(np.abs(gf[k] - of[k]).max()))
+        assert g.rng_state() == o.rng.state
+
+
 # -------------------------------------------------------------- live oracle
 
 @pytest.mark.parametrize("spec", [(128, 128, 8, 8), (37, 5, 2, 10), (2, 1, 2, 2), (70, 129, 2, 6), (24, 257, 4, 12)])
@@ -266,6 +286,10 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(gen_compact=1, gen_split=2), dict(ycoop=3), dict(ycoop=2, nt_loads=0), dict(zsplit=1),
                 dict(zsplit=1, nt_loads=0), dict(zsplit=0), dict(ycoop=4), dict(ycoop=4, nt_loads=0),
                 dict(ycoop=7), dict(ycoop=8, nt_loads=0), dict(ycoop=7, ycoop_ovh=64), dict(ycoop_ovh=0),
+                dict(ycoop=7, ycoop_order=1), dict(ycoop=7, ycoop_order=4), dict(ycoop=8, ycoop_order=16), dict(ycoop_order=0),
+                dict(ycoop=7, ycoop_map=1), dict(ycoop=8, ycoop_map=1), dict(ycoop_map=0),
+                dict(ycoop=0, rows_per_wave=1, yunroll=16), dict(ycoop=0, rows_per_wave=2, yunroll=32),
+                dict(ycoop=0, rows_per_wave=2, yunroll=16, nt_loads=1), dict(yunroll=2),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),

@@ -75,8 +75,10 @@ struct CompDev {
 };
 
 struct PhaseEvents {
-    hipEvent_t e[6]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end
+    hipEvent_t e[8]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end, and the
+                     // prefetched y-pass's start and end (ypre)
     bool rng = false;
+    bool ypre = false;
 };
 
 } // namespace
@@ -172,6 +174,11 @@ struct df_handle {
     int nsets = 2;
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
+    // y-pass prefetch (ypre): the next call's y-pass depends only on its noise (not on dt), so it is enqueued
+    // on rng_stream right after that noise and runs beside this call's z-pass; df_filter then runs the
+    // z-pass only. ydone[set]: the generation in that set already holds its y-filtered r_zs interior.
+    int ypre = 0;
+    bool ydone[kMaxNoiseSets] = {};
     RngGeom geom{};
     // halo
     double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
@@ -383,6 +390,7 @@ int drain_profile(df_handle *h)
         for (int p = 0; p < 3; ++p) (void)hipEventElapsedTime(&t[p], h->ev[i].e[p], h->ev[i].e[p + 1]);
         (void)hipEventElapsedTime(&tot, h->ev[i].e[0], h->ev[i].e[3]);
         if (h->ev[i].rng) (void)hipEventElapsedTime(&r, h->ev[i].e[4], h->ev[i].e[5]);
+        if (h->ev[i].ypre) (void)hipEventElapsedTime(&t[0], h->ev[i].e[6], h->ev[i].e[7]); // on rng_stream
         h->prof.rng_ms += r;
         h->prof.ypass_ms += t[0];
         h->prof.halo_ms += t[1];
@@ -390,6 +398,7 @@ int drain_profile(df_handle *h)
         h->prof.total_ms += tot;
         h->prof.calls++;
         h->ev[i].rng = false;
+        h->ev[i].ypre = false;
     }
     h->ev_used = 0;
     return DF_OK;
@@ -441,6 +450,17 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     return DF_OK;
 }
 
+// ypre applies to single-plane handles (no strips: the halo exchange sits between the two passes)
+bool ypre_active(const df_handle *h) { return h->ypre && h->world == 1 && !h->group; }
+
+// A visible step's y-pass, unless the generation it consumes already ran it (ypre).
+int phase_ypass(df_handle *h, int comps_mask);
+int ypass_unless_done(df_handle *h)
+{
+    if (h->ydone[h->cur]) return DF_OK;
+    return phase_ypass(h, 7);
+}
+
 int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
     const long long gi = h->gen_launched;
@@ -452,6 +472,22 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
                              h->rng_blocks, nb_scan, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5);
+    const int set = gen_set(h, gi);
+    h->ydone[set] = false;
+    if (ypre_active(h)) { // this generation's y-pass, under the current call's z-pass
+        const int saved = h->cur;
+        h->cur = set;
+        SweepArgs a = sweep_args(h);
+        h->cur = saved;
+        a.comps_mask = 7;
+        if (prof_on(h)) ev_record(h, 6);
+        HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, rs), DF_EHIP);
+        if (prof_on(h)) {
+            ev_record(h, 7);
+            h->ev[h->ev_used].ypre = true;
+        }
+        h->ydone[set] = true;
+    }
     if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
     h->gen_launched++;
@@ -854,6 +890,8 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_ABLATE_HANDOFF")) h->ablate_handoff = std::atoi(e);
     h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
+    h->ypre = 0;
+    if (const char *e = std::getenv("DFAMD_YPRE")) h->ypre = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -1341,7 +1379,7 @@ int step0(df_handle *h)
     // Constructor step 0 (df.cpp:57-62): noise, sweeps, RST; no correlation, no SRA.
     int rc;
     if ((rc = consume_gen(h))) return rc;
-    if ((rc = phase_ypass(h, 7))) return rc;
+    if ((rc = ypass_unless_done(h))) return rc;
     if ((rc = phase_halo_rccl(h))) return rc;
     if ((rc = phase_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
@@ -1393,7 +1431,7 @@ void drop_graphs(df_handle *h)
 // enqueued, no per-call events (profiling), no CSV, no RCCL.
 bool graph_ok(df_handle *h)
 {
-    return h->use_graph && h->hb == 1 && h->nsets == 2 && h->overlap && h->world == 1 && !h->group && !h->profiling &&
+    return h->use_graph && !h->ypre && h->hb == 1 && h->nsets == 2 && h->overlap && h->world == 1 && !h->group && !h->profiling &&
            !h->halo_loopback && h->csv_path.empty() && h->gen_launched == h->gen_used + 1;
 }
 
@@ -1619,7 +1657,7 @@ int df_filter(df_handle *h, double dt)
     const bool prof = prof_on(h);
     if ((rc = consume_gen(h))) return rc;
     ev_record(h, 0);
-    if ((rc = phase_ypass(h, 7))) return rc;
+    if ((rc = ypass_unless_done(h))) return rc;
     ev_record(h, 1);
     if ((rc = phase_halo_rccl(h))) return rc;
     ev_record(h, 2);
@@ -1978,6 +2016,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             }
         }
     }
+    else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
     else if (k == "ycoop_map") {
         if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");
         h->ycoop_map = value;

@@ -1266,6 +1266,59 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
+    if (TABLE && !PC && YU < 4 && a.ydeep && a.ywindow && Nlo == Nhi && t + 7 <= bh) {
+        // The same deep pipeline on a tile whose R rows share one N (row-uniform planes, every tile but
+        // where N steps): tap t of row r uses b[t - r] of ONE vector, so a group's 4 taps x R rows need
+        // the R + 3 coefficients b[t - R + 1 .. t + 3], one scalar window (s_load_dwordx16 at R = 4)
+        // instead of R row loads and their address arithmetic. Same products, same order: bit-identical.
+        constexpr int WN = (R + 3 + 7) / 8 * 8;
+        const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
+        double2 nA[4], nB[4];
+        double wA[WN], wB[WN];
+        // running pointers (noise row t0, window of t0), advanced by a group per load: no per-group multiplies
+        const double *nq = np + (ptrdiff_t)t * Pz, *wq = cb + t;
+        const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
+        auto ld = [&](int, double2 (&nn)[4], double (&ww)[WN]) {
+            nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nq), 0);
+            nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P1), 1);
+            nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P2), 2);
+            nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P3), 3);
+#pragma unroll
+            for (int k = 0; k < WN; ++k) ww[k] = DF_TCOEF(wq[k]); // the table is padded past its last vector
+            nq += P4;
+            wq += 4;
+        };
+        auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const double b = ww[u - r + R - 1];
+                    acc0[r] += b * nn[u].x;
+                    acc1[r] += b * nn[u].y;
+                }
+        };
+        ld(t, nA, wA);
+        for (; t + 11 <= bh; t += 8) {
+            ld(t + 4, nB, wB);
+            __builtin_amdgcn_sched_barrier(0);
+            taps(nA, wA);
+            __builtin_amdgcn_sched_barrier(0);
+            ld(t + 8, nA, wA);
+            __builtin_amdgcn_sched_barrier(0);
+            taps(nB, wB);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (t + 7 <= bh) {
+            ld(t + 4, nB, wB);
+            taps(nA, wA);
+            taps(nB, wB);
+            t += 8;
+        } else {
+            taps(nA, wA);
+            t += 4;
+        }
+    }
     if (TABLE && !PC && YU < 4 && a.ydeep && t + 7 <= bh) {
         // Table mode, deep pipeline (SweepArgs::ydeep): taps go in groups of 4 noise rows; the next
         // group's noise (4 x 16 B per lane) and coefficients (R x 4 scalars) are loaded a whole group

@@ -290,6 +290,9 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ycoop=7, ycoop_map=1), dict(ycoop=8, ycoop_map=1), dict(ycoop_map=0),
                 dict(ycoop=0, rows_per_wave=1, yunroll=16), dict(ycoop=0, rows_per_wave=2, yunroll=32),
                 dict(ycoop=0, rows_per_wave=2, yunroll=16, nt_loads=1), dict(yunroll=2),
+                dict(ypre=1), dict(ypre=1, handoff_batch=2), dict(ypre=1, graph=1), dict(ypre=0),
+                dict(ydeep=1, ywindow=0), dict(ydeep=1, ywindow=1, rows_per_wave=2), dict(ywindow=1, rows_per_wave=8),
+                dict(ywindow=1, rows_per_wave=1), dict(ywindow=1, rows_per_wave=4),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
@@ -329,6 +332,37 @@ def test_handoff_batch_mid_epoch_state_changes(monkeypatch, hb):
         if i == 2:  # mid-epoch: restart the pipeline from the oracle's current state
             st = o.rng.state
             g.set_rng_state(*st)
+        assert g.rng_state() == o.rng.state, i
+        for k in FIELDS:
+            assert np.array_equal(g.field(k), o.field(k)), (i, k)
+
+
+@pytest.mark.parametrize("mode", ["table", "packed"])
+@pytest.mark.parametrize("hb", ["1", "2"])
+def test_ypass_prefetch_matches_oracle(monkeypatch, mode, hb):
+    # ypre: the next call's y-pass runs on the RNG stream right after its noise. Filter calls, a stream state set
+    # mid-run, the stage API and a switch of the knob itself, all against the oracle after every step
+    monkeypatch.setenv("DFAMD_YPRE", "1")
+    monkeypatch.setenv("DFAMD_HANDOFF_BATCH", hb)
+    spec = (48, 96, 2, 10)
+    o = oracle_synth(*spec, seed=17)
+    g = gpu_synth(*spec, seed=17, coeff_mode=mode)
+    for i in range(8):
+        if i == 5:  # stage API: one component's sweeps redo its y-pass on the consumed set (same bits)
+            o.generate_white_noise()
+            g.generate_white_noise()
+            for c in range(3):
+                o.filtering_sweeps(c)
+                g.filtering_sweeps(c)
+            continue
+        o.filter(1e-8)
+        g.filter(1e-8)
+        if i == 2:
+            g.set_rng_state(*o.rng.state)
+        if i == 3:
+            g.set_tuning("ypre", 0)
+        if i == 6:
+            g.set_tuning("ypre", 1)
         assert g.rng_state() == o.rng.state, i
         for k in FIELDS:
             assert np.array_equal(g.field(k), o.field(k)), (i, k)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# y-pass prefetch (ypre): the next call's y-pass on the RNG stream beside this call's z-pass. Parity, then
+# same-handle A/B (ypre 0 vs 1) on c3/c2/native in table mode and c3/native packed.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out/r3x
+mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py \
+  -k "ypass_prefetch or runtime_tuning or native or handoff or stage" > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for cm in "c3 table" "c2 table" "native table" "c1 table" "c3 packed" "native packed"; do
+  set -- $cm
+  timeout -k 10 200 python3 tools/ab.py --config $1 --mode $2 --rounds 9 --calls 20 --tune-a ypre=0 --tune-b ypre=1 \
+    > $O/ab_$1_$2.json || { echo "ab failed"; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/ab_$1_$2.json'));print('$1 $2 ypre0', d['A_median_ms'], 'ypre1', d['B_median_ms'])"
+done

@@ -120,6 +120,7 @@ struct df_handle {
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
+    int zocc = 0;        // z-pass register budget (SweepArgs::zocc)
     int ycoop_map = 0;   // row-pair y-pass tiles to XCDs: 0 equal-byte contiguous runs, 1 interleaved (t % 8)
     int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
                          // consecutive tiles, heaviest group first (balance_ycoop2)
@@ -326,6 +327,7 @@ SweepArgs sweep_args(df_handle *h)
         a.ycoop2_perm[c] = h->ycoop_order ? h->c[c].ycoop2_perm : nullptr;
     }
     a.ycoop2_map = h->ycoop_map;
+    a.zocc = h->zocc;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -2017,6 +2019,8 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         }
     }
     else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
+    else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
+
     else if (k == "ycoop_map") {
         if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");
         h->ycoop_map = value;

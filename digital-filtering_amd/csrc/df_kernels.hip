@@ -857,8 +857,13 @@ __device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q
     store_pair(g, e.d0, e.d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
 }
 
+#if defined(DF_K3A_WPE)
+#define DF_K3A_ATTR __attribute__((amdgpu_waves_per_eu(DF_K3A_WPE)))
+#else
+#define DF_K3A_ATTR
+#endif
 template <int kDenseG> // chunks per K3a wave (RngGeom::dense_g: 4, 8 or 16)
-__global__ __launch_bounds__(kRngThreads) void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+__global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                         RngStateDev *__restrict__ sout)
 {
     __shared__ Near1Slot stack_all[kRngThreads / 64][128]; // < 64 carried + 64 pushed per chunk
@@ -1121,8 +1126,13 @@ __device__ __forceinline__ void write_window(int T, int W)
 // i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
 // coalesced dwordx4 per (row, tap).
 
+#if defined(DF_YPASS_WPE)
+#define DF_YPASS_ATTR __attribute__((amdgpu_waves_per_eu(DF_YPASS_WPE)))
+#else
+#define DF_YPASS_ATTR
+#endif
 template <int R, bool TABLE, bool NT, int YU, bool PC>
-__global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
+__global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, int nrowblk)
 {
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
@@ -1290,13 +1300,17 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         };
         auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const double b = ww[u - r + R - 1];
                     acc0[r] += b * nn[u].x;
                     acc1[r] += b * nn[u].y;
                 }
+                // one tap's products at a time: the scheduler would otherwise compute a whole group's
+                // products first (123 -> 105 VGPRs; c3 table call -2%, profiles/r3/aa)
+                __builtin_amdgcn_sched_barrier(0);
+            }
         };
         ld(t, nA, wA);
         for (; t + 11 <= bh; t += 8) {
@@ -1336,12 +1350,14 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
         };
         auto taps = [&](const double2 (&nn)[4], const double (&cc)[R][4]) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     acc0[r] += cc[r][u] * nn[u].x;
                     acc1[r] += cc[r][u] * nn[u].y;
                 }
+                __builtin_amdgcn_sched_barrier(0); // as above
+            }
         };
         ld(t, nA, cA);
         for (; t + 11 <= bh; t += 8) {
@@ -1837,8 +1853,10 @@ __device__ __forceinline__ void zstage_copy(const SweepArgs &a, double *lds, int
     }
 }
 
-template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false>
-__global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
+// WPE: the register budget as waves per SIMD (amdgpu_waves_per_eu; 1 = the compiler's choice, 76 VGPRs and 6
+// waves here; 8 = 54-64 VGPRs, SweepArgs::zocc)
+template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void zpass_kernel(SweepArgs a)
 {
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
@@ -2076,14 +2094,18 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
         const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
-        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
+        if (u4 && a.zocc >= 8)
+            hipLaunchKernelGGL((zpass_kernel<true, false, 4, false, false, 8>), dim3(blocks), dim3(256), lds, st, a);
+        else if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
     } else if (a.zsplit) { // packed, one 3-wave block per tile
         const unsigned b3 = (unsigned)tiles;
         if (a.nt_loads) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
         else hipLaunchKernelGGL((zpass_kernel<false, false, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
     } else if (a.nt_loads) {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
+        if (u4 && a.zocc >= 8)
+            hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, false, 8>), dim3(blocks), dim3(256), 0, st, a);
+        else if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);
     } else {
         if (u4) hipLaunchKernelGGL((zpass_kernel<false, false, 4, false>), dim3(blocks), dim3(256), 0, st, a);

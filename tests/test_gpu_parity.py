@@ -292,7 +292,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ycoop=0, rows_per_wave=2, yunroll=16, nt_loads=1), dict(yunroll=2),
                 dict(ypre=1), dict(ypre=1, handoff_batch=2), dict(ypre=1, graph=1), dict(ypre=0),
                 dict(ydeep=1, ywindow=0), dict(ydeep=1, ywindow=1, rows_per_wave=2), dict(ywindow=1, rows_per_wave=8),
-                dict(ywindow=1, rows_per_wave=1), dict(ywindow=1, rows_per_wave=4),
+                dict(ywindow=1, rows_per_wave=1), dict(ywindow=1, rows_per_wave=4), dict(zocc=8), dict(zocc=0),
+                dict(zocc=8, zunroll=2),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),

@@ -180,6 +180,7 @@ struct df_handle {
     // z-pass only. ydone[set]: the generation in that set already holds its y-filtered r_zs interior.
     int ypre = 0;
     bool ydone[kMaxNoiseSets] = {};
+    int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
     RngGeom geom{};
     // halo
     double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
@@ -433,6 +434,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
     g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? 1 : 0;
+    if (!h->k3a_fast) g.chunk_dest[0] = g.chunk_dest[1] = nullptr;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
@@ -894,6 +896,7 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
     h->ypre = 0;
     if (const char *e = std::getenv("DFAMD_YPRE")) h->ypre = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_K3A_FAST")) h->k3a_fast = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -1299,9 +1302,35 @@ int alloc_dense(df_handle *h)
         for (uint64_t c = 0; c < nch; ++c)
             if ((bits[f][c >> 5] >> (c & 31)) & 1u) list[f].push_back((uint32_t)c);
     }
+    // K3a fast chunks (one GPU): all 128 positions in one r_ys array (every column stored), at most one row wrap,
+    // every rank live and none the call's last (that one sets the stream state): destinations by arithmetic
+    std::vector<ChunkDest> dest[2];
+    for (int f = 0; f < 2; ++f) {
+        const long long A = (long long)((g.Q - f + 1) / 2);
+        dest[f].resize(std::max<size_t>(1, list[f].size()), ChunkDest{0, 0, 0, -1, 0});
+        for (size_t i = 0; i < list[f].size(); ++i) {
+            const uint64_t c = list[f][i], q0 = f + 128 * c;
+            if ((long long)(64 * c + 63) >= A - 1) continue;
+            int su = 0;
+            while (su < 5 && q0 >= g.seg[su + 1]) ++su;
+            const uint64_t W = g.width[su];
+            if ((su & 1) || g.z0 != 0 || g.z1 != g.Nz_g || W < 128 || q0 + 128 > g.seg[su + 1]) continue;
+            const uint64_t p = q0 - g.seg[su], row = p / W, col = p % W;
+            ChunkDest d{};
+            d.off = (long long)(row * (uint64_t)g.Pz + col);
+            d.wr = (short)std::min<uint64_t>(128, W - col);
+            d.jump = g.Pz - (int)W;
+            d.arr = (signed char)su;
+            dest[f][i] = d;
+        }
+    }
     int rc;
     uint32_t *db[2], *dl[2];
     for (int f = 0; f < 2; ++f) {
+        ChunkDest *dd = nullptr;
+        if ((rc = dalloc_t(h, &dd, dest[f].size()))) return rc;
+        if ((rc = upload(h, dd, dest[f].data(), dest[f].size()))) return rc;
+        h->geom.chunk_dest[f] = dd;
         if ((rc = dalloc_t(h, &db[f], bits[f].size()))) return rc;
         if ((rc = upload(h, db[f], bits[f].data(), bits[f].size()))) return rc;
         if ((rc = dalloc_t(h, &dl[f], std::max<size_t>(1, list[f].size())))) return rc;
@@ -2019,6 +2048,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         }
     }
     else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
+    else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
 
     else if (k == "ycoop_map") {

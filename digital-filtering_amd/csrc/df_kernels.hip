@@ -884,6 +884,43 @@ __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_ke
         // the next chunk's states are in flight while this chunk computes
         const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
         const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
+        const ChunkDest cd = g.chunk_dest[f] && !g.debug_flags ? g.chunk_dest[f][i0 + k] : ChunkDest{0, 0, 0, -1, 0};
+        if (cd.arr >= 0) { // uniform
+            // fast chunk (host-built ChunkDest): every lane live and not the call's last attempt, both positions
+            // in one r_ys array - no stream position search, no per-lane destination branches
+            double *const base = (cd.arr == 0 ? g.ry[0] : cd.arr == 2 ? g.ry[1] : g.ry[2]) + cd.off;
+            const int e0 = 2 * lane;
+            double *const p0 = base + e0 + (e0 >= cd.wr ? cd.jump : 0);
+            double *const p1 = base + e0 + 1 + (e0 + 1 >= cd.wr ? cd.jump : 0);
+            uint64_t s3f;
+            const PolarAttempt af = polar_draws(s, s3f);
+            const bool nearf = defer && glibc_log_near1(af.r2);
+            const uint64_t nmf = __ballot(nearf);
+            if (nmf) {
+                if (nearf) {
+                    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nmf >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)nmf, 0u));
+                    stk[top + below] = Near1Slot{af.x, af.y, p0, p1};
+                }
+                top += __popcll(nmf);
+            }
+            if (!nearf) {
+                const double lg = defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
+                const double mult = sqrt(-2 * lg / af.r2);
+                const double xm = af.x * mult;
+                const double ym = af.y * mult;
+                store_pair(g, p0, p1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+            }
+            if (top >= 64) { // as below
+                __asm__ volatile("" ::: "memory");
+                near1_batch(g, stk, top, 64, lane);
+                top -= 64;
+                __asm__ volatile("" ::: "memory");
+            }
+            c = cn;
+            s = sn;
+            continue;
+        }
         const long long rank = c * 64 + lane;
         const uint64_t q = f + 2ull * (uint64_t)rank;
         const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform

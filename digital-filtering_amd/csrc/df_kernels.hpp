@@ -49,6 +49,16 @@ struct WaveTask {
     int gw, pad;
 };
 
+// K3a destination of a 128-position chunk (host-built, RngGeom::chunk_dest): position i of the chunk goes to
+// r_ys[arr >> 1] + off + i, plus jump once i >= wr (the row wrap: pitch - width).
+struct ChunkDest {
+    long long off;
+    int jump;
+    short wr;
+    signed char arr; // even: r_ys of component arr >> 1; -1: general path
+    signed char pad;
+};
+
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
@@ -83,6 +93,9 @@ struct RngGeom {
     const uint32_t *need_bits[2];   // bitmap over chunks (+ 2 padding words), per parity f
     const uint32_t *chunks[2];      // needed chunk ids in increasing order, per parity f
     int nchunks[2];
+    // K3a fast chunks (one GPU): per listed chunk, where its 128 positions land when they all go to one r_ys
+    // array with at most one row wrap; arr < 0 marks a chunk for the general per-lane path.
+    const struct ChunkDest *chunk_dest[2];
 };
 
 struct SweepArgs {

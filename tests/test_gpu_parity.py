@@ -293,7 +293,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ypre=1), dict(ypre=1, handoff_batch=2), dict(ypre=1, graph=1), dict(ypre=0),
                 dict(ydeep=1, ywindow=0), dict(ydeep=1, ywindow=1, rows_per_wave=2), dict(ywindow=1, rows_per_wave=8),
                 dict(ywindow=1, rows_per_wave=1), dict(ywindow=1, rows_per_wave=4), dict(zocc=8), dict(zocc=0),
-                dict(zocc=8, zunroll=2),
+                dict(zocc=8, zunroll=2), dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=0),
+                dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=1),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
@@ -336,6 +337,26 @@ def test_handoff_batch_mid_epoch_state_changes(monkeypatch, hb):
         assert g.rng_state() == o.rng.state, i
         for k in FIELDS:
             assert np.array_equal(g.field(k), o.field(k)), (i, k)
+
+
+@pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90), (37, 129, 2, 10), (40, 133, 2, 8)])
+def test_dense_fast_chunks_match_oracle(spec):
+    # K3a's fast chunks (host-built destinations, ChunkDest) forced through the dense generation on small planes:
+    # odd and even widths (row wraps inside a chunk, odd wrap points), both parities of the carried normal
+    o = oracle_synth(*spec, seed=29)
+    g = gpu_synth(*spec, seed=29, coeff_mode="table")
+    for k, v in (("gen_split", 1), ("fuse_plan", 0), ("gen_dense", 1)):
+        g.set_tuning(k, v)
+    flags = set()
+    for i in range(5):
+        o.filter(1e-8)
+        g.filter(1e-8)
+        st = g.rng_state()
+        flags.add(st[1])
+        assert st == o.rng.state, i
+        for k in FIELDS:
+            assert np.array_equal(g.field(k), o.field(k)), (i, k)
+    print("saved flags seen:", sorted(flags))
 
 
 @pytest.mark.parametrize("mode", ["table", "packed"])

@@ -214,7 +214,13 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * "gen_split" (1,2,4,8,16: noise-generation waves per wave of attempts), "fuse_plan" (planes of
  * <= 1024 attempt blocks: K3 plans its own waves, one launch fewer; default 1 in table mode and on packed
  * planes without long y chains, 0 on packed planes that use the row-pair y-pass), "graph" (steady-state
- * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling). */
+ * single-GPU calls replayed as one HIP graph; default off - measured slower - never while profiling).
+ * Round 3: "ycoop_order" (row-pair y-pass dispatch inside each XCD run: 0 ascending rows, g >= 1 groups of g
+ * tiles heaviest first; default 4 on long-chain packed planes), "ycoop_map" (1: row-pair tiles interleaved
+ * over the XCDs), "yunroll" 16 / 32 (packed per-wave y-pass register rings of 1-2 rows), "ypre" (the next
+ * call's y-pass on the RNG stream beside this call's z-pass; one GPU), "zocc" (8: z-pass register budget
+ * for 8 waves per SIMD) - these four measured neutral or slower and are off - and
+ * "k3a_fast" (default 1; 0: every K3a chunk through the general destination path). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every

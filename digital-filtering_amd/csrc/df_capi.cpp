@@ -121,6 +121,7 @@ struct df_handle {
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
     int zocc = 0;        // z-pass register budget (SweepArgs::zocc)
+    int ydepth = 1;      // table y-pass, 1-2 rows per wave: 16 noise rows in flight (SweepArgs::ydepth)
     int ycoop_map = 0;   // row-pair y-pass tiles to XCDs: 0 equal-byte contiguous runs, 1 interleaved (t % 8)
     int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
                          // consecutive tiles, heaviest group first (balance_ycoop2)
@@ -329,6 +330,7 @@ SweepArgs sweep_args(df_handle *h)
     }
     a.ycoop2_map = h->ycoop_map;
     a.zocc = h->zocc;
+    a.ydepth = h->ydepth;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -855,13 +857,15 @@ int plan_strips(df_handle *h)
     // Default launch shapes, measured on MI355X (tools/tune_sweep.py, tools/ab.py; profiles/r1/probe/
     // tune_small_planes.jsonl): c3-class planes packed 2 rows per wave, table 4. Where a wave's serial tap chain
     // rather than bandwidth sets the time - y half-widths >= 128 (the reference's own grid: 212) or
-    // under ~1 wave per SIMD - packed takes 1 row with the 8-deep load pipeline, table 2 rows.
+    // under ~1 wave per SIMD - packed takes 1 row with the 8-deep load pipeline, table 1 row (round 3).
     if (h->rows_per_wave == 0) {
         int nymax = 0;
         for (int c = 0; c < 3; ++c) nymax = std::max(nymax, s.comp[c].Ny_max);
         const bool long_chain = nymax >= 128;
         const bool tiny = (long long)h->nstrips * ((s.Ny + 1) / 2) < 1024;
-        if (h->coeff_mode == DF_COEFF_TABLE) h->rows_per_wave = long_chain ? 2 : 4;
+        // table mode, long chains: 1 row per wave with the noise 4 groups ahead (ydepth): the reference's grid
+        // -4..-7% per call against 2 rows (profiles/r3/ao)
+        if (h->coeff_mode == DF_COEFF_TABLE) h->rows_per_wave = long_chain ? 1 : 4;
         else if (long_chain || tiny) {
             h->rows_per_wave = 1;
             if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
@@ -2050,6 +2054,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
+    else if (k == "ydepth") h->ydepth = value != 0;
 
     else if (k == "ycoop_map") {
         if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");

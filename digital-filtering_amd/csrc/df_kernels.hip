@@ -1313,6 +1313,71 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
+    if constexpr (TABLE && !PC && YU < 4 && R <= 2) {
+        // Long chains (table mode takes 1-2 rows per wave where N_y >= 128, the reference's grid: up to 426
+        // taps per wave at ~3 waves per SIMD): the wave's serial chain of noise-row loads sets the time, so
+        // the noise runs kYD groups of 4 rows ahead in a register ring (16 rows in flight instead of 4-8);
+        // the group's coefficient window is a scalar load one group ahead. Same products, same order.
+        constexpr int kYD = 4;
+        constexpr int WN = (R + 3 + 7) / 8 * 8;
+        if (a.ydeep && a.ywindow && a.ydepth && Nlo == Nhi && t + 4 * kYD - 1 <= bh) {
+            const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
+            double2 nq[kYD][4];
+            const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
+            const double *nl = np + (ptrdiff_t)t * Pz; // next group to load
+            auto ldn = [&](double2 (&nn)[4]) {
+                nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nl), 0);
+                nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P1), 1);
+                nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P2), 2);
+                nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P3), 3);
+                nl += P4;
+            };
+            auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        const double b = ww[u - r + R - 1];
+                        acc0[r] += b * nn[u].x;
+                        acc1[r] += b * nn[u].y;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            };
+            const double *wq = cb + t;
+            double w[WN];
+#pragma unroll
+            for (int k = 0; k < WN; ++k) w[k] = DF_TCOEF(wq[k]);
+#pragma unroll
+            for (int g = 0; g < kYD; ++g) ldn(nq[g]);
+            for (; t + 8 * kYD - 1 <= bh; t += 4 * kYD) { // the groups issued below stay within bh
+#pragma unroll
+                for (int g = 0; g < kYD; ++g) {
+                    double wn[WN];
+#pragma unroll
+                    for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]); // the table is padded past its last vector
+                    __builtin_amdgcn_sched_barrier(0);
+                    taps(nq[g], w);
+                    ldn(nq[g]); // group t + 4 (g + kYD)
+                    __builtin_amdgcn_sched_barrier(0);
+                    wq += 4;
+#pragma unroll
+                    for (int k = 0; k < WN; ++k) w[k] = wn[k];
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < kYD; ++g) { // drain: groups t .. t + 4 kYD - 1, loaded, within bh
+                double wn[WN];
+#pragma unroll
+                for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]);
+                taps(nq[g], w);
+                wq += 4;
+#pragma unroll
+                for (int k = 0; k < WN; ++k) w[k] = wn[k];
+            }
+            t += 4 * kYD;
+        }
+    }
     if (TABLE && !PC && YU < 4 && a.ydeep && a.ywindow && Nlo == Nhi && t + 7 <= bh) {
         // The same deep pipeline on a tile whose R rows share one N (row-uniform planes, every tile but
         // where N steps): tap t of row r uses b[t - r] of ONE vector, so a group's 4 taps x R rows need

@@ -135,6 +135,7 @@ struct SweepArgs {
     const int *ycoop2_perm[3]; // dispatch position -> tile inside each run (nullptr: ascending)
     int ycoop2_map;            // 0: XCD x runs tiles [ycoop2_xcd[c][x], ...); 1: tile t on XCD t % 8 (interleaved)
     int zocc;                  // z-pass register budget: 0 the compiler's (6 waves per SIMD), 8 (8 waves, zpass WPE)
+    int ydepth;                // table y-pass at 1-2 rows per wave: noise 4 groups of 4 rows ahead (1) or 1-2 (0)
     int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
     int ydeep;              // table y-pass: noise and coefficients loaded a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)

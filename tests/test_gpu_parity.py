@@ -164,7 +164,7 @@ def test_golden_native_grid(mode, tuning):
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=8)), ("packed", dict(ycoop_order=1)),
                                          ("packed", dict(ycoop_order=8)), ("packed", dict(ycoop_map=1)),
-                                         ("table", {})])
+                                         ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
     # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
@@ -294,7 +294,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(ydeep=1, ywindow=0), dict(ydeep=1, ywindow=1, rows_per_wave=2), dict(ywindow=1, rows_per_wave=8),
                 dict(ywindow=1, rows_per_wave=1), dict(ywindow=1, rows_per_wave=4), dict(zocc=8), dict(zocc=0),
                 dict(zocc=8, zunroll=2), dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=0),
-                dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=1),
+                dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=1), dict(ydepth=0, rows_per_wave=2),
+                dict(ydepth=1, rows_per_wave=2), dict(ydepth=1, rows_per_wave=1), dict(ydepth=1, rows_per_wave=4),
                 dict(ydeep=1), dict(ydeep=1, rows_per_wave=8), dict(ydeep=1, rows_per_wave=2),
                 dict(ydeep=1, rows_per_wave=1), dict(ydeep=0), dict(ydeep=1), dict(fuse_plan=0),
                 dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),

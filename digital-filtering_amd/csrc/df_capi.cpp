@@ -1379,15 +1379,18 @@ int build(df_handle *h, const df_config_c *cfg)
     // Hand-off batch: small single-GPU planes, where the two per-call cross-stream hand-offs are 10-40% of
     // a call (c2 packed -17%, the reference's grid -9%, c1 -40% with both removed; profiles/r3/h), take
     // epochs of hb calls over 2*hb noise sets (a few MB each there): c1 (16k cells) 4, c2 (262k) 2
-    // (c1 -23% packed / -15% table, c2 -6% / -9%; profiles/r3/i/hb_ab.jsonl). Not on planes with long y
-    // chains: the reference's grid ran +3% packed / +14% table with epochs (its latency-bound y-pass reads
-    // noise written calls earlier, no longer cache-warm), so it keeps one hand-off per call, as do split
-    // planes and RCCL handles (their RNG exchanges stay in call order with the halo).
+    // (c1 -23% packed / -15% table, c2 -6% / -9%; profiles/r3/i/hb_ab.jsonl). Planes with long y chains
+    // (the reference's grid) ran slower with epochs in round 2 (+3% packed / +14% table: their latency-bound
+    // y-pass read noise written calls earlier, no longer cache-warm); with round 3's y-passes (row-pair
+    // dispatch order, table at 1 row per wave with a deep noise ring) epochs of 4 pay there too: -3..-4%
+    // packed, -5..-6% table (profiles/r3/at; c2 keeps 2, c1 4: r3/au). Split planes and RCCL handles keep
+    // one hand-off per call (their RNG exchanges stay in call order with the halo).
     {
         int nymax = 0;
         for (int c = 0; c < 3; ++c) nymax = std::max(nymax, h->setup.comp[c].Ny_max);
         const long long cells = (long long)h->Ny * h->Nz_loc;
-        if (h->world == 1 && !cfg->comm_id && nymax < 128) h->hb = cells <= (1ll << 16) ? 4 : cells <= (1ll << 20) ? 2 : 1;
+        if (h->world == 1 && !cfg->comm_id)
+            h->hb = cells <= (1ll << 16) || (nymax >= 128 && cells <= (1ll << 20)) ? 4 : cells <= (1ll << 20) ? 2 : 1;
     }
     if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_HB_BURST")) h->hb_burst = std::atoi(e);

@@ -804,6 +804,22 @@ __global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom 
     const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
     uint64_t st = thread_first_state(g, sin->state, b, tid);
     long long R = r_lo; // uniform: rank of this iteration's first accepted attempt
+    if (need == ((2u << span) - 1u)) {
+        // every chunk of the wave's ranks is needed (one GPU: all but the r_zs interior's): no per-iteration
+        // chunk tests; the wave's accepted attempts hold exactly the ranks [r_lo, r_lo + nw)
+#pragma unroll 4
+        for (int m = 0; m < kRngPerThread; ++m) {
+            const bool acc = (bits >> m) & 1u;
+            const uint64_t mask = __ballot(acc);
+            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+            const long long rank = R + below;
+            if (acc && rank < A) g.cstate[rank] = st;
+            R += __popcll(mask);
+            st = g.next_mult * st + g.next_plus;
+        }
+        return;
+    }
 #pragma unroll 4
     for (int m = 0; m < kRngPerThread; ++m) {
         const bool acc = (bits >> m) & 1u;

@@ -172,6 +172,12 @@ struct df_handle {
     // profiles/r3/h). With hb > 1 the generations go in epochs of hb calls over 2*hb noise sets: one
     // noise-ready wait and one release record on the sweep stream per epoch instead of per call.
     int hb = 1;
+    // the configured hand-off batch; a stream state loaded from outside (df_set_rng_state: checkpoints, the C++
+    // objects of one process handing the reference's shared stream on) drops to one generation per epoch, so a
+    // program that switches objects every call regenerates one generation per switch, not hb; after
+    // kHbRestoreCalls calls without such a load the handle returns to hb_conf
+    int hb_conf = 1;
+    int calls_since_load = 0;
     int hb_burst = 0; // 1: an epoch's generations enqueued in one burst (measured against spread, profiles/r3/m)
     int nsets = 2;
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
@@ -414,6 +420,8 @@ int drain_profile(df_handle *h)
 // Epochs of the noise pipeline: with hb == 1 every generation is its own epoch (absolute index, so the
 // event parity is the noise-set parity, as the graph path assumes); with hb > 1, epochs of hb
 // generations counted from gen_base.
+constexpr int kHbRestoreCalls = 16;
+
 long long gen_epoch(const df_handle *h, long long g) { return h->hb == 1 ? g : (g - h->gen_base) / h->hb; }
 int gen_pos(const df_handle *h, long long g) { return h->hb == 1 ? 0 : (int)((g - h->gen_base) % h->hb); }
 int gen_set(const df_handle *h, long long g) { return (int)(g % h->nsets); }
@@ -1396,6 +1404,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_HB_BURST")) h->hb_burst = std::atoi(e);
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
+    h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
@@ -1680,6 +1689,8 @@ df_handle *df_create(const df_config_c *cfg)
     return h;
 }
 
+static int restart_pipeline(df_handle *h, int hb_new);
+
 int df_filter(df_handle *h, double dt)
 {
     if (!valid_dev(h)) return DF_EINVAL;
@@ -1688,6 +1699,9 @@ int df_filter(df_handle *h, double dt)
     if (h->world > 1 && !h->comm && !h->solo_strip)
         return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    if (h->hb != h->hb_conf && ++h->calls_since_load > kHbRestoreCalls) { // no state loads lately: batch again
+        if ((rc = sync_all(h)) || (rc = restart_pipeline(h, h->hb_conf))) return rc;
+    }
     if (graph_ok(h)) return graph_call(h, dt);
     // Sampled phase events: each hipEventRecord is a queue packet between this call's kernels, and on
     // short calls six of them cost up to 10% of the call (tools/event_cost.py; profiles/r3/d)
@@ -2015,8 +2029,9 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
     HIP_OR(hipMemcpyAsync(h->rstate + gen_set(h, h->gen_used), &st, sizeof st, hipMemcpyHostToDevice, h->stream),
            DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
-    if (h->gen_launched > h->gen_used) // the prefetched noise came from the old state: redo it
-        return restart_pipeline(h, h->hb);
+    h->calls_since_load = 0;
+    if (h->gen_launched > h->gen_used || h->hb != 1) // the prefetched noise came from the old state: redo it
+        return restart_pipeline(h, 1);
     return DF_OK;
 }
 
@@ -2104,6 +2119,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
                                        " (DFAMD_HANDOFF_BATCH at create)");
         if (value > 1 && (h->world > 1 || h->comm || h->group))
             return fail(DF_EINVAL, "handoff_batch > 1 is for single-GPU handles");
+        h->hb_conf = value;
         if (h->device >= 0 && value != h->hb) {
             int rc = sync_all(h);
             if (rc) return rc;

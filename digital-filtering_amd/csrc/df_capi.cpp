@@ -164,6 +164,12 @@ struct df_handle {
     ncclComm_t rng_comm = nullptr;           // second communicator: the count all-gather runs on rng_stream
     hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
     hipEvent_t ev_halo = nullptr;            // split counting: the halo of the call just enqueued is done
+    // RCCL z-strips (round 3): the halo send/recv, the unpack and the edge strips' z-pass run on comm_stream
+    // (high priority) while the stream runs the z-pass of the strips whose stencils stay inside this rank's
+    // columns (phase_halo_zpass). 0 = one serial chain (pack, send/recv, unpack, whole z-pass).
+    int halo_overlap = 1;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_packed = nullptr, ev_unpacked = nullptr; // halo packed (stream); edge strips done (comm_stream)
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
     long long gen_launched = 0; // generations enqueued (generation n reads state slot n%nsets, writes (n+1)%nsets)
     long long gen_used = 0;     // generations consumed by a visible step (ctor step 0, filter, stage API)
@@ -310,6 +316,9 @@ SweepArgs sweep_args(df_handle *h)
     a.Nz_loc = h->Nz_loc;
     a.Pz = h->Pz;
     a.nstrips = h->nstrips;
+    a.zs_lo = 0;
+    a.zs_n = a.zs_gap_at = h->nstrips;
+    a.zs_gap = 0;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
     a.tabf = h->tabf;
@@ -388,6 +397,7 @@ int sync_all(df_handle *h)
 {
     HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    if (h->comm_stream) HIP_OR(hipStreamSynchronize(h->comm_stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -634,12 +644,12 @@ int phase_halo_pack(df_handle *h)
     return DF_OK;
 }
 
-int phase_halo_unpack(df_handle *h)
+int phase_halo_unpack(df_handle *h, hipStream_t st = nullptr)
 {
     if (h->world == 1) return DF_OK;
     SweepArgs a = sweep_args(h);
     HIP_OR(launch_halo_unpack(a, h->rank > 0 ? h->recv_l : nullptr, h->rank < h->world - 1 ? h->recv_r : nullptr,
-                              h->stream),
+                              st ? st : h->stream),
            DF_EHIP);
     return DF_OK;
 }
@@ -664,30 +674,93 @@ int halo_loopback(df_handle *h)
     return DF_OK;
 }
 
+// The grouped send/recv with rank +- 1 on stream st, then ev_halo there.
+int halo_sendrecv(df_handle *h, hipStream_t st)
+{
+    NCCL_OR(ncclGroupStart());
+    if (h->rank > 0) {
+        NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
+        NCCL_OR(ncclRecv(h->recv_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
+    }
+    if (h->rank < h->world - 1) {
+        NCCL_OR(ncclSend(h->send_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, st));
+        NCCL_OR(ncclRecv(h->recv_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, st));
+    }
+    NCCL_OR(ncclGroupEnd());
+    if (h->ev_halo) HIP_OR(hipEventRecord(h->ev_halo, st), DF_EHIP);
+    return DF_OK;
+}
+
 int phase_halo_rccl(df_handle *h)
 {
     if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
     if (h->solo_strip) return DF_OK;
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
     int rc = phase_halo_pack(h);
-    if (rc) return rc;
-    NCCL_OR(ncclGroupStart());
-    if (h->rank > 0) {
-        NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, h->stream));
-        NCCL_OR(ncclRecv(h->recv_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, h->stream));
-    }
-    if (h->rank < h->world - 1) {
-        NCCL_OR(ncclSend(h->send_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, h->stream));
-        NCCL_OR(ncclRecv(h->recv_r, h->halo_elems, ncclDouble, h->rank + 1, h->comm, h->stream));
-    }
-    NCCL_OR(ncclGroupEnd());
-    if (h->ev_halo) HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
+    if (rc || (rc = halo_sendrecv(h, h->stream))) return rc;
     return phase_halo_unpack(h);
 }
 
-int phase_zpass(df_handle *h, bool corr, bool sra, double dt)
+// Strips [lo, hi) of a z-strip rank read no halo column: strip s spans columns [128 s, 128 s + 127] and its
+// stencils reach Nzp further either side (Nzp = the widest component's Nz_max), so it is interior when
+// 128 s >= Nzp and 128 (s + 1) + Nzp <= Nz_loc. The plane's own edges (rank 0's left, the last rank's right)
+// read the generated raw-noise pads (df.cpp:385-405's quirk), not the halo, so they count as interior.
+bool halo_interior(const df_handle *h, int *lo, int *hi)
+{
+    int w = 0;
+    for (int c = 0; c < 3; ++c) w = std::max(w, h->c[c].Nzp);
+    *lo = h->rank == 0 ? 0 : (w + kStrip - 1) / kStrip;
+    *hi = h->rank == h->world - 1 ? h->nstrips : std::max(0, (h->Nz_loc - w) / kStrip);
+    *hi = std::min(*hi, h->nstrips);
+    return *hi > *lo;
+}
+
+int phase_zpass(df_handle *h, bool corr, bool sra, double dt, int part = 0, hipStream_t st = nullptr);
+
+// Halo exchange, then the z-pass. RCCL z-strips with halo_overlap: the stream packs the halo and runs the
+// z-pass of the interior strips; comm_stream (high priority) runs the send/recv, the unpack and the edge
+// strips' z-pass beside it, and the stream waits for that before the call ends. The edge strips' blocks
+// join the interior launch's as its slots free instead of running as a small launch on an idle chip (the
+// round-1 form, which also split the y-pass, lost 80-190 us per call that way; profiles/r1/probe/
+// halo_overlap_rejected.jsonl).
+int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
+{
+    int lo = 0, hi = 0, rc;
+    if (h->world == 1 || h->solo_strip || !h->comm || !h->halo_overlap || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
+        if ((rc = phase_halo_rccl(h))) return rc;
+        ev_record(h, 2);
+        return phase_zpass(h, corr, sra, dt);
+    }
+    if ((rc = phase_halo_pack(h))) return rc;
+    HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
+    ev_record(h, 2); // halo_ms is the pack alone here; the exchange runs under zpass_ms
+    HIP_OR(hipStreamWaitEvent(h->comm_stream, h->ev_packed, 0), DF_EHIP);
+    if ((rc = halo_sendrecv(h, h->comm_stream))) return rc;
+    if ((rc = phase_halo_unpack(h, h->comm_stream))) return rc;
+    if ((rc = phase_zpass(h, corr, sra, dt, 2, h->comm_stream))) return rc; // edge strips
+    HIP_OR(hipEventRecord(h->ev_unpacked, h->comm_stream), DF_EHIP);
+    if ((rc = phase_zpass(h, corr, sra, dt, 1))) return rc; // interior strips
+    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_unpacked, 0), DF_EHIP);
+    return DF_OK;
+}
+
+// part 0: every strip; 1: the halo-interior strips; 2: the edge strips around them (halo_interior)
+int phase_zpass(df_handle *h, bool corr, bool sra, double dt, int part, hipStream_t st)
 {
     SweepArgs a = sweep_args(h);
+    if (part) {
+        int lo = 0, hi = 0;
+        halo_interior(h, &lo, &hi);
+        if (part == 1) {
+            a.zs_lo = lo;
+            a.zs_n = a.zs_gap_at = hi - lo;
+        } else {
+            a.zs_n = lo + (h->nstrips - hi);
+            a.zs_gap_at = lo;
+            a.zs_gap = hi - lo;
+            a.zstage = 0; // a block's 4 tiles may straddle the gap
+        }
+    }
     if (corr) {
         const double pi = 3.141592654; // df.cpp:411
         for (int c = 0; c < 3; ++c) {
@@ -698,7 +771,7 @@ int phase_zpass(df_handle *h, bool corr, bool sra, double dt)
     }
     a.do_corr = corr ? 1 : 0;
     a.do_sra = sra ? 1 : 0;
-    HIP_OR(launch_zpass(a, h->coeff_mode == DF_COEFF_TABLE, h->stream), DF_EHIP);
+    HIP_OR(launch_zpass(a, h->coeff_mode == DF_COEFF_TABLE, st ? st : h->stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -1372,6 +1445,14 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         HIP_OR(hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
         h->split_count = !h->rng_replicate;
+        if (h->world > 1) {
+            int prio_lo = 0, prio_hi = 0;
+            HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
+            HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
+            HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
+            HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
+        }
+        if (const char *e = std::getenv("DFAMD_HALO_OVERLAP")) h->halo_overlap = std::atoi(e);
     }
     return DF_OK;
 }
@@ -1427,8 +1508,7 @@ int step0(df_handle *h)
     int rc;
     if ((rc = consume_gen(h))) return rc;
     if ((rc = ypass_unless_done(h))) return rc;
-    if ((rc = phase_halo_rccl(h))) return rc;
-    if ((rc = phase_zpass(h, false, false, 0.0))) return rc;
+    if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
     if ((rc = sync_all(h))) return rc;
     return check_rng_error(h);
@@ -1459,6 +1539,9 @@ void destroy(df_handle *h)
         if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
     }
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream), (void)hipStreamDestroy(h->comm_stream);
+    if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
+    if (h->ev_unpacked) (void)hipEventDestroy(h->ev_unpacked);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }
@@ -1711,9 +1794,7 @@ int df_filter(df_handle *h, double dt)
     ev_record(h, 0);
     if ((rc = ypass_unless_done(h))) return rc;
     ev_record(h, 1);
-    if ((rc = phase_halo_rccl(h))) return rc;
-    ev_record(h, 2);
-    if ((rc = phase_zpass(h, true, true, dt))) return rc;
+    if ((rc = phase_halo_zpass(h, true, true, dt))) return rc; // phase event 2 inside
     ev_record(h, 3);
     if ((rc = prefetch_gen(h))) return rc; // next call's noise, under this call's sweeps
     if (prof) h->ev_used++;
@@ -2073,6 +2154,11 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
     else if (k == "ydepth") h->ydepth = value != 0;
+    else if (k == "halo_overlap") {
+        if (h->device >= 0)
+            if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
+        h->halo_overlap = value != 0;
+    }
 
     else if (k == "ycoop_map") {
         if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");

@@ -1979,10 +1979,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
     const int tile = SPLIT ? (int)blockIdx.x : uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
-    const int Ny = a.Ny;
-    if (tile >= a.nstrips * Ny) return; // block-uniform when SPLIT
-    int j = tile / a.nstrips;
-    const int s = tile - j * a.nstrips;
+    const int Ny = a.Ny, nst = a.zs_n; // this launch's strips (SweepArgs::zs_lo ...)
+    if (tile >= nst * Ny) return; // block-uniform when SPLIT
+    int j = tile / nst;
+    const int sl = tile - j * nst;
+    const int s = a.zs_lo + sl + (sl >= a.zs_gap_at ? a.zs_gap : 0);
     if (a.heavy_first) j = Ny - 1 - j;
     const int col = s * kStrip + 2 * lane;
 
@@ -1991,10 +1992,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // the waves read their tap pairs from there (ds_read_b128) instead of 4 overlapping
     // (128 + 2N)-column windows through L1. Block-uniform: the barrier is reached by all.
     bool staged = false;
-    if (TABLE && !PC && a.zstage) {
+    if (TABLE && !PC && a.zstage) { // (launches with a strip gap run unstaged: zstage 0)
         const int t0 = blockIdx.x * 4;
-        staged = t0 + 3 < a.nstrips * Ny && t0 / a.nstrips == (t0 + 3) / a.nstrips;
-        const int s0 = t0 - (t0 / a.nstrips) * a.nstrips;
+        staged = t0 + 3 < nst * Ny && t0 / nst == (t0 + 3) / nst;
+        const int s0 = a.zs_lo + t0 - (t0 / nst) * nst;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             if (!staged || !((a.comps_mask >> c) & 1)) continue;
@@ -2205,7 +2206,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
 {
-    const long long tiles = (long long)a.nstrips * a.Ny;
+    const long long tiles = (long long)a.zs_n * a.Ny;
+    if (tiles <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
     const bool u4 = a.zunroll >= 4;
     if (table && a.per_cell) {

@@ -25,6 +25,8 @@ def main():
     h = dfamd.DigitalFilter(rank=rank, world=world, comm_id=bytes.fromhex(spec["comm_id"]), **plane)
     if "replicate" in spec:  # 1: every rank counts the whole stream; 0: split counting + the counts all-gather
         h.set_tuning("rng_replicate", int(spec["replicate"]))
+    if "halo_overlap" in spec:  # 0: pack, send/recv, unpack and the whole z-pass as one chain on the stream
+        h.set_tuning("halo_overlap", int(spec["halo_overlap"]))
     for dt in spec["dts"]:
         h.filter(dt)
     h.sync()

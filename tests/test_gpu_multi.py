@@ -37,14 +37,14 @@ def emulated_host_env(rank):
 
 
 def run_world(world, mode, replicate, Ny=256, Nz=1024, N_min=4, N_max=32, seed=11, dts=(1e-8, 1e-8, 1e-5),
-              emulate=False):
+              emulate=False, extra=None):
     sys.path.insert(0, os.path.join(ROOT, "digital-filtering_amd"))
     import dfamd
     cid = dfamd.comm_unique_id().hex()  # the bootstrap root lives in this process until the ranks join
     procs = []
     for r in range(world):
         spec = dict(rank=r, world=world, comm_id=cid, Ny=Ny, Nz=Nz, N_min=N_min, N_max=N_max, seed=seed,
-                    mode=mode, replicate=replicate, dts=list(dts), device=0 if emulate else r)
+                    mode=mode, replicate=replicate, dts=list(dts), device=0 if emulate else r, **(extra or {}))
         procs.append(subprocess.Popen([sys.executable, WORKER, json.dumps(spec)], stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True, start_new_session=True,
                                       env=emulated_host_env(r) if emulate else None))
@@ -92,3 +92,16 @@ def test_rccl_strips_emulated_hosts(world, mode, replicate):
         pytest.skip("needs a GPU")
     outs = run_world(world, mode, replicate, emulate=True)
     check_world(outs, world, replicate)
+
+
+@pytest.mark.parametrize("world,Nz", [(2, 1024), (3, 1000), (4, 2048)])
+@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 0)])
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
+    """Both halo forms bit-equal to the unsplit plane: the exchange under the interior strips' z-pass (the
+    default; N_max 64 leaves 1-3 interior strips per rank here) and the serial chain (halo_overlap 0)."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(world, mode, replicate, Nz=Nz, N_min=4, N_max=64, emulate=True,
+                     extra=dict(halo_overlap=overlap))
+    check_world(outs, world, replicate, Nz=Nz)

@@ -166,8 +166,12 @@ struct df_handle {
     hipEvent_t ev_halo = nullptr;            // split counting: the halo of the call just enqueued is done
     // RCCL z-strips (round 3): the halo send/recv, the unpack and the edge strips' z-pass run on comm_stream
     // (high priority) while the stream runs the z-pass of the strips whose stencils stay inside this rank's
-    // columns (phase_halo_zpass). 0 = one serial chain (pack, send/recv, unpack, whole z-pass).
-    int halo_overlap = 1;
+    // columns (phase_halo_zpass). 0 = one serial chain (pack, send/recv, unpack, whole z-pass). -1 (default):
+    // packed planes only. One rank of c4 over 8 timed alone without the exchange (profiles/r3/az): packed
+    // 1.83-1.85 vs 1.85-1.92 ms (the split costs nothing, so the exchange time is the gain); table 0.296-0.308
+    // vs 0.278-0.290 ms (+17 us: a row of 6 interior strips leaves half the 4-tile blocks unstaged and the
+    // edge launch runs unstaged, against an exchange of a few tens of us).
+    int halo_overlap = -1;
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_packed = nullptr, ev_unpacked = nullptr; // halo packed (stream); edge strips done (comm_stream)
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
@@ -694,7 +698,7 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
 int phase_halo_rccl(df_handle *h)
 {
     if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
-    if (h->solo_strip) return DF_OK;
+    if (h->solo_strip) return phase_halo_pack(h); // timing only: the pack, no exchange
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
     int rc = phase_halo_pack(h);
     if (rc || (rc = halo_sendrecv(h, h->stream))) return rc;
@@ -726,7 +730,9 @@ int phase_zpass(df_handle *h, bool corr, bool sra, double dt, int part = 0, hipS
 int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
 {
     int lo = 0, hi = 0, rc;
-    if (h->world == 1 || h->solo_strip || !h->comm || !h->halo_overlap || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
+    const bool peer = h->comm && !h->solo_strip; // DFAMD_SOLO_STRIP (timing only): the same streams, no exchange
+    const bool ov = h->halo_overlap > 0 || (h->halo_overlap < 0 && h->coeff_mode == DF_COEFF_PACKED);
+    if (h->world == 1 || !(peer || h->solo_strip) || !ov || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
         if ((rc = phase_halo_rccl(h))) return rc;
         ev_record(h, 2);
         return phase_zpass(h, corr, sra, dt);
@@ -735,8 +741,8 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
     ev_record(h, 2); // halo_ms is the pack alone here; the exchange runs under zpass_ms
     HIP_OR(hipStreamWaitEvent(h->comm_stream, h->ev_packed, 0), DF_EHIP);
-    if ((rc = halo_sendrecv(h, h->comm_stream))) return rc;
-    if ((rc = phase_halo_unpack(h, h->comm_stream))) return rc;
+    if (peer && (rc = halo_sendrecv(h, h->comm_stream))) return rc;
+    if (peer && (rc = phase_halo_unpack(h, h->comm_stream))) return rc;
     if ((rc = phase_zpass(h, corr, sra, dt, 2, h->comm_stream))) return rc; // edge strips
     HIP_OR(hipEventRecord(h->ev_unpacked, h->comm_stream), DF_EHIP);
     if ((rc = phase_zpass(h, corr, sra, dt, 1))) return rc; // interior strips
@@ -1445,13 +1451,13 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         HIP_OR(hipEventCreateWithFlags(&h->ev_halo, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventRecord(h->ev_halo, h->stream), DF_EHIP);
         h->split_count = !h->rng_replicate;
-        if (h->world > 1) {
-            int prio_lo = 0, prio_hi = 0;
-            HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
-            HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
-            HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
-            HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
-        }
+    }
+    if (h->world > 1 && (cfg->comm_id || h->solo_strip)) {
+        int prio_lo = 0, prio_hi = 0;
+        HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
+        HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
+        HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
+        HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
         if (const char *e = std::getenv("DFAMD_HALO_OVERLAP")) h->halo_overlap = std::atoi(e);
     }
     return DF_OK;
@@ -2157,7 +2163,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
-        h->halo_overlap = value != 0;
+        h->halo_overlap = value < 0 ? -1 : value != 0;
     }
 
     else if (k == "ycoop_map") {

@@ -221,9 +221,9 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * call's y-pass on the RNG stream beside this call's z-pass; one GPU), "zocc" (8: z-pass register budget
  * for 8 waves per SIMD) - these four measured neutral or slower and are off - and
  * "k3a_fast" (default 1; 0: every K3a chunk through the general destination path),
- * "halo_overlap" (RCCL z-strips, default 1: the halo send/recv and unpack on a high-priority stream
- * under the z-pass of the strips that read no halo column, the edge strips after it; 0: one serial
- * chain). */
+ * "halo_overlap" (RCCL z-strips: 1 = the halo send/recv, the unpack and the edge strips' z-pass on a
+ * high-priority stream under the z-pass of the strips that read no halo column; 0 = one serial chain;
+ * -1, the default = 1 on packed planes, 0 in table mode). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every

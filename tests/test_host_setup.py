@@ -150,7 +150,7 @@ def test_c_abi_rejects_bad_arguments():
     assert L.df_set_tuning(native._h, b"ycoop_ovh", 64) == 0
     # round-3 keys: the dispatch order re-plans device tables only on handles that have them
     for key, val in ((b"ycoop_order", 4), (b"ycoop_order", 0), (b"ycoop_map", 1), (b"ypre", 1), (b"zocc", 8),
-                     (b"k3a_fast", 0), (b"ydepth", 0), (b"yunroll", 32), (b"halo_overlap", 0)):
+                     (b"k3a_fast", 0), (b"ydepth", 0), (b"yunroll", 32), (b"halo_overlap", 0), (b"halo_overlap", -1)):
         assert L.df_set_tuning(native._h, key, val) == 0, key
     assert L.df_set_tuning(native._h, b"ycoop_order", -1) == -1
     assert L.df_set_tuning(native._h, b"ycoop_map", 2) == -1

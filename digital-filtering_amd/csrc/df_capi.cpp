@@ -195,6 +195,7 @@ struct df_handle {
     // y-pass prefetch (ypre): the next call's y-pass depends only on its noise (not on dt), so it is enqueued
     // on rng_stream right after that noise and runs beside this call's z-pass; df_filter then runs the
     // z-pass only. ydone[set]: the generation in that set already holds its y-filtered r_zs interior.
+    int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds)
     int ypre = 0;
     bool ydone[kMaxNoiseSets] = {};
     int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
@@ -350,6 +351,7 @@ SweepArgs sweep_args(df_handle *h)
     a.ycoop2_map = h->ycoop_map;
     a.zocc = h->zocc;
     a.ydepth = h->ydepth;
+    a.ylds = h->ylds;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -957,6 +959,10 @@ int plan_strips(df_handle *h)
             h->rows_per_wave = 1;
             if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
         } else h->rows_per_wave = 2;
+        // table mode, long chains: the noise staged in LDS per block of 4 rows, 2 chunks in flight (ylds): the
+        // reference's grid y-pass 0.051 -> 0.043 ms, call -9%; c3 and c2 (short chains, FP64-issue-bound) lose
+        // with it (profiles/r3/bd)
+        if (h->coeff_mode == DF_COEFF_TABLE && long_chain && !std::getenv("DFAMD_YLDS")) h->ylds = 2;
         // Long chains, packed: one block per row pair, noise loads shared by both rows, the next chunk in
         // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
         // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
@@ -987,6 +993,7 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
     h->ypre = 0;
     if (const char *e = std::getenv("DFAMD_YPRE")) h->ypre = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_YLDS")) h->ylds = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_K3A_FAST")) h->k3a_fast = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
@@ -2124,6 +2131,23 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
 
 long long df_stream_length(df_handle *h) { return valid(h) ? (long long)h->geom.Q : -1; }
 
+int df_get_tuning(df_handle *h, const char *key, int *value)
+{
+    if (!h || !key || !value) return fail(DF_EINVAL, "null handle, key or value");
+    const std::string k(key);
+    const std::pair<const char *, int> keys[] = {
+        {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"zunroll", h->zunroll},
+        {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ycoop_map", h->ycoop_map}, {"ydepth", h->ydepth},
+        {"ylds", h->ylds}, {"ypre", h->ypre}, {"zocc", h->zocc}, {"handoff_batch", h->hb_conf},
+        {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"k3a_fast", h->k3a_fast}};
+    for (const auto &kv : keys)
+        if (k == kv.first) {
+            *value = kv.second;
+            return DF_OK;
+        }
+    return fail(DF_EINVAL, "unknown tuning key for df_get_tuning: " + k);
+}
+
 int df_set_tuning(df_handle *h, const char *key, int value)
 {
     // Launch-shape knobs only: every setting produces bit-identical fields (tests/test_gpu_parity.py).
@@ -2160,6 +2184,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
     else if (k == "ydepth") h->ydepth = value != 0;
+    else if (k == "ylds") h->ylds = value < 0 ? 0 : value > 3 ? 3 : value; // noise chunks in flight (0: off)
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with

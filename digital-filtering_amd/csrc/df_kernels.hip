@@ -12,6 +12,8 @@
 //
 // All FP64 and built with -ffp-contract=off: every product and sum rounds on its
 // own, in the reference's order, so the sweeps are bit-exact given equal noise.
+#include <type_traits>
+
 #include "df_kernels.hpp"
 #include "df_rng.hpp"
 
@@ -1833,8 +1835,157 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     }
 }
 
+// K4 table mode, noise staged in LDS (SweepArgs::ylds): one block per (strip, 4R rows), wave w summing rows
+// j0 + wR .. j0 + wR + R - 1 for the lane's column pair. The block walks the union of its rows' noise ranges
+// in chunks of 16 noise rows: every noise row is read from global memory ONCE per block (each wave loads 4 of
+// the chunk's rows, the next chunk's loads in flight through the current chunk's sums) and from LDS by every
+// wave whose rows reach it. The per-wave forms load each noise row once per wave: on c3 their 2.6 GB of
+// vector-memory reads per call hold the y-pass 0.05 ms above its FP64 floor (ablation, profiles/r3/an).
+// Each row adds its taps in the order i = -N..N (noise rows ascending), so results are bit-identical.
+template <int K> using ic_t = std::integral_constant<int, K>;
+
+// PD: chunks of noise loads in flight (register sets; the loop is unrolled by PD so each set stays static)
+template <int R, int PD>
+__global__ __launch_bounds__(256) void ypass_tlds_kernel(SweepArgs a, int nrowblk)
+{
+    constexpr int C = 16; // noise rows per chunk
+    __shared__ double2 nbuf[2][C][64];
+    const int c = blockIdx.y;
+    if (!((a.comps_mask >> c) & 1)) return;
+    const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
+    const int per_xcd = gridDim.x >> 3; // XCD-aware: each XCD a contiguous run of strip-major tiles
+    const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= a.nstrips * nrowblk) return; // block-uniform
+    const int s = tile / nrowblk;
+    int rb = tile - s * nrowblk;
+    if (a.heavy_first) rb = nrowblk - 1 - rb;
+    const int Ny = a.Ny, RB = 4 * R, j0 = rb * RB;
+    const int *nst = a.Ny_st[c] + (size_t)s * Ny;
+    int mlo = 1 << 30, mhi = -(1 << 30); // the block's noise rows
+    for (int q = 0; q < RB && j0 + q < Ny; ++q) {
+        const int N = nst[j0 + q];
+        mlo = min(mlo, j0 + q - N);
+        mhi = max(mhi, j0 + q + N);
+    }
+    const int jw = j0 + w * R;
+    int lo[R], hi[R];
+    const double *tb[R]; // row r's full tap vector: tap t = m - lo[r] at tb[r][t]
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        lo[r] = 1 << 30;
+        hi[r] = -(1 << 30);
+        tb[r] = a.tabf;
+        if (jw + r < Ny) {
+            const int N = nst[jw + r];
+            lo[r] = jw + r - N;
+            hi[r] = jw + r + N;
+            tb[r] = a.tabf + a.tabf_off[N];
+        }
+    }
+    const int col = s * kStrip + 2 * lane;
+    const bool live = col < a.Nz_loc;
+    const double *np = a.ry[c] + (size_t)a.Nyp[c] * a.Pz + col; // noise row m at np + m * Pz
+    double2 pre[PD][4];
+    auto gload = [&](auto K, int u0) {
+        constexpr int k0 = decltype(K)::value;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int m = u0 + w + 4 * k;
+            pre[k0][k] = live && m <= mhi ? DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)m * a.Pz), m)
+                                          : make_double2(0.0, 0.0);
+        }
+    };
+    auto lstore = [&](auto K, int buf) {
+        constexpr int k0 = decltype(K)::value;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nbuf[buf][w + 4 * k][lane] = pre[k0][k];
+    };
+    double acc0[R], acc1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0.0;
+    auto compute = [&](int u0, int buf) {
+        const int mb = min(u0 + C - 1, mhi);
+        bool full = mb == u0 + C - 1, any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            full = full && lo[r] <= u0 && hi[r] >= mb;
+            any = any || (lo[r] <= mb && hi[r] >= u0);
+        }
+        if (full) { // every row of the wave takes all 16 noise rows of the chunk
+            const double *cb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) cb[r] = tb[r] + (u0 - lo[r]);
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                const double2 n = nbuf[buf][q][lane];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const double b = DF_TCOEF(cb[r][q]);
+                    acc0[r] += b * n.x;
+                    acc1[r] += b * n.y;
+                }
+            }
+        } else if (any) {
+            for (int m = u0; m <= mb; ++m) {
+                const double2 n = nbuf[buf][m - u0][lane];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (m >= lo[r] && m <= hi[r]) { // wave-uniform
+                        const double b = DF_TCOEF(tb[r][m - lo[r]]);
+                        acc0[r] += b * n.x;
+                        acc1[r] += b * n.y;
+                    }
+            }
+        }
+    };
+    // chunk i: rows mlo + 16 i ..; its loads in register set i % PD, its sums from LDS buffer i % 2.
+    // Step i: the loads of chunk i + PD go into the set chunk i vacated, chunk i is summed, chunk i + 1
+    // (loaded PD - 1 steps earlier) is stored to the other buffer, barrier.
+    const int nch = (mhi - mlo) / C + 1;
+    gload(ic_t<0>{}, mlo);
+    if constexpr (PD > 1) gload(ic_t<1 % PD>{}, mlo + C);
+    if constexpr (PD > 2) gload(ic_t<2 % PD>{}, mlo + 2 * C);
+    lstore(ic_t<0>{}, 0);
+    __syncthreads();
+    auto step = [&](auto K, int i) {
+        constexpr int k = decltype(K)::value;
+        if (i + PD < nch) gload(K, mlo + (i + PD) * C); // block-uniform
+        compute(mlo + i * C, i & 1);
+        if (i + 1 < nch) lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+        __syncthreads();
+    };
+    for (int i = 0; i < nch; i += PD) {
+        step(ic_t<0>{}, i);
+        if constexpr (PD > 1)
+            if (i + 1 < nch) step(ic_t<1 % PD>{}, i + 1);
+        if constexpr (PD > 2)
+            if (i + 2 < nch) step(ic_t<2 % PD>{}, i + 2);
+    }
+    write_window(a.ywin_T, a.ywin_W);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (jw + r >= Ny) continue;
+        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.Nzp[c] + col;
+        if (col + 1 < a.Nz_loc) {
+            if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
+            else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
+        } else if (col < a.Nz_loc) o[0] = acc0[r];
+    }
+}
+
 template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
 {
+    if constexpr (TABLE) {
+        if (a.ylds && !a.per_cell) {
+            const int nrowblk = (a.Ny + 4 * R - 1) / (4 * R);
+            const unsigned blocks = (unsigned)(((long long)a.nstrips * nrowblk + 7) / 8 * 8);
+            // 4 and 8 rows per wave take one chunk in flight: with 2-3 the compiler puts their arrays in scratch
+            if (R <= 2 && a.ylds >= 3) hipLaunchKernelGGL((ypass_tlds_kernel<R <= 2 ? R : 1, 3>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            else if (R <= 2 && a.ylds == 2) hipLaunchKernelGGL((ypass_tlds_kernel<R <= 2 ? R : 1, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            else hipLaunchKernelGGL((ypass_tlds_kernel<R, 1>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            return hipGetLastError();
+        }
+    }
     const int nrowblk = (a.Ny + R - 1) / R;
     const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle

@@ -110,6 +110,7 @@ def lib():
         "df_plane_info": (C.c_int, [H, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
         "df_set_profiling": (C.c_int, [H, C.c_int]),
         "df_set_tuning": (C.c_int, [H, C.c_char_p, C.c_int]),
+        "df_get_tuning": (C.c_int, [H, C.c_char_p, C.POINTER(C.c_int)]),
         "df_gather_field": (C.c_int, [H, C.c_int, C.c_longlong, C.c_void_p, C.c_void_p, C.c_void_p, C.c_longlong,
                                       C.c_double]),
         "df_get_profile": (C.c_int, [H, C.POINTER(Profile)]),
@@ -374,6 +375,12 @@ class DigitalFilter:
     # --- measurement
     def set_tuning(self, key, value):
         _check(lib().df_set_tuning(self._h, key.encode(), int(value)))
+
+    def get_tuning(self, key):
+        """The launch shape in use for a tuning key (plane-dependent defaults or the last set_tuning)."""
+        v = C.c_int(0)
+        _check(lib().df_get_tuning(self._h, key.encode(), C.byref(v)))
+        return v.value
 
     def set_profiling(self, on, every=1):
         """on: phase events on; every n > 1: only on every n-th filter() call (sampled)."""

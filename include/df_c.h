@@ -226,6 +226,12 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * -1, the default = 1 on packed planes, 0 in table mode). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
+/* The launch shape the handle will use for a df_set_tuning key: the plane-dependent defaults chosen at
+ * create time (host-only handles included) or the last setting. Keys: "rows_per_wave", "yunroll",
+ * "zunroll", "ycoop", "ycoop_order", "ycoop_map", "ydepth", "ylds", "ypre", "zocc", "handoff_batch",
+ * "halo_overlap", "gen_dense", "k3a_fast". DF_EINVAL for other keys. */
+int df_get_tuning(df_handle *h, const char *key, int *value);
+
 /* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every
  * n-th df_filter only (the first of each n; df_profile.calls counts the timed calls): the events are
  * queue packets between a call's kernels and cost up to 10% of a short call. */

@@ -164,7 +164,9 @@ def test_golden_native_grid(mode, tuning):
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=8)), ("packed", dict(ycoop_order=1)),
                                          ("packed", dict(ycoop_order=8)), ("packed", dict(ycoop_map=1)),
-                                         ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1))])
+                                         ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1)),
+                                         ("table", dict(ylds=1)), ("table", dict(ylds=2, rows_per_wave=2)),
+                                         ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
     # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
@@ -302,7 +304,10 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0, gen_split=1, gen_dense=1), dict(dense_g=4), dict(dense_g=32), dict(dense_g=128),
                 dict(count_grid=3), dict(count_grid=0, dense_g=16), dict(gen_dense=0), dict(gen_dense=1, dense_g=8),
                 dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4), dict(handoff_batch=2, graph=1),
-                dict(handoff_batch=1, graph=1), dict(graph=0, handoff_batch=4)]
+                dict(handoff_batch=1, graph=1), dict(graph=0, handoff_batch=4), dict(ylds=1, rows_per_wave=1),
+                dict(ylds=2, rows_per_wave=2), dict(ylds=3, rows_per_wave=4), dict(ylds=1, rows_per_wave=8),
+                dict(ylds=2, rows_per_wave=1), dict(ylds=3, rows_per_wave=1), dict(ylds=2, rows_per_wave=8),
+                dict(ylds=1, heavy_first=0), dict(ylds=0, heavy_first=1)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -364,7 +369,8 @@ def test_dense_fast_chunks_match_oracle(spec):
 
 def test_random_planes_bitexact_vs_oracle():
     # seeded random plane shapes and half-width ranges, both coefficient modes, table mode also through the
-    # dense generation (fast chunks) and the packed mode through the row-pair y-pass with its dispatch orders:
+    # dense generation (fast chunks) and the LDS-staged y-pass (ylds), the packed mode through the row-pair y-pass
+    # with its dispatch orders:
     # every field bit for bit against the oracle after step 0 and two calls
     rs = np.random.RandomState(2024)
     for case in range(10):
@@ -376,7 +382,10 @@ def test_random_planes_bitexact_vs_oracle():
         hs = {"packed": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="packed"),
               "table": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="table"),
               "dense": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="table"),
-              "coop2": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="packed")}
+              "coop2": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="packed"),
+              "tlds": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="table")}
+        hs["tlds"].set_tuning("ylds", int(rs.choice([1, 2, 3])))
+        hs["tlds"].set_tuning("rows_per_wave", int(rs.choice([1, 2, 4])))
         for k, v in (("gen_split", 1), ("fuse_plan", 0), ("gen_dense", 1)):
             hs["dense"].set_tuning(k, v)
         hs["coop2"].set_tuning("ycoop", 7)

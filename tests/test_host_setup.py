@@ -317,3 +317,26 @@ def test_alloc_registry_rejects_overlapping_ranges():
     assert L.df_alloc_registry_count() == n0
     assert L.df_alloc_registry(base + 0x800, 0x1000, 1) == 0  # free again after release
     assert L.df_alloc_registry(base + 0x800, 0, 0) == 0
+
+
+@pytest.mark.parametrize("plane,mode,expect", [
+    # the reference's grid (y half-widths up to 212): table 1 row per wave + LDS-staged noise, epochs of 4;
+    # packed the row-pair y-pass in heaviest-first groups of 4
+    (dict(), "table", dict(rows_per_wave=1, ylds=2, handoff_batch=4, ycoop=0)),
+    (dict(), "packed", dict(rows_per_wave=1, ycoop=7, ycoop_order=4, ylds=0, handoff_batch=4)),
+    # c3 (half-widths 4-64): table 4 rows per wave, no LDS staging, one hand-off per call; packed 2 rows
+    (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "table",
+     dict(rows_per_wave=4, ylds=0, handoff_batch=1, ycoop=0, gen_dense=1)),
+    (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "packed",
+     dict(rows_per_wave=2, ylds=0, ycoop=0, handoff_batch=1)),
+    # c2: epochs of 2
+    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(rows_per_wave=4, ylds=0, handoff_batch=2)),
+])
+def test_launch_plan_defaults(plane, mode, expect):
+    # the plane-dependent launch shapes chosen at create time (df_get_tuning on host-only handles): a change to
+    # the planning rules shows here before it shows as a slower bench line
+    f = host(coeff_mode=mode, **plane)
+    got = {k: f.get_tuning(k) for k in expect}
+    assert got == expect
+    with pytest.raises(dfamd.DFError, match="unknown tuning"):
+        f.get_tuning("warp_size")

@@ -196,6 +196,7 @@ struct df_handle {
     // on rng_stream right after that noise and runs beside this call's z-pass; df_filter then runs the
     // z-pass only. ydone[set]: the generation in that set already holds its y-filtered r_zs interior.
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds)
+    int ylds_nw = 4, ylds_ch = 16;
     int ypre = 0;
     bool ydone[kMaxNoiseSets] = {};
     int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
@@ -352,6 +353,8 @@ SweepArgs sweep_args(df_handle *h)
     a.zocc = h->zocc;
     a.ydepth = h->ydepth;
     a.ylds = h->ylds;
+    a.ylds_nw = h->ylds_nw;
+    a.ylds_ch = h->ylds_ch;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -2185,6 +2188,8 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
     else if (k == "ydepth") h->ydepth = value != 0;
     else if (k == "ylds") h->ylds = value < 0 ? 0 : value > 3 ? 3 : value; // noise chunks in flight (0: off)
+    else if (k == "ylds_nw") h->ylds_nw = value == 8 ? 8 : 4;
+    else if (k == "ylds_ch") h->ylds_ch = value == 32 ? 32 : 16;
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with

@@ -1845,10 +1845,11 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
 template <int K> using ic_t = std::integral_constant<int, K>;
 
 // PD: chunks of noise loads in flight (register sets; the loop is unrolled by PD so each set stays static)
-template <int R, int PD>
-__global__ __launch_bounds__(256) void ypass_tlds_kernel(SweepArgs a, int nrowblk)
+// NW waves per block (one block = NW R rows), C noise rows per chunk (C / NW loaded per wave)
+template <int R, int PD, int NW = 4, int C = 16>
+__global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nrowblk)
 {
-    constexpr int C = 16; // noise rows per chunk
+    constexpr int LW = C / NW; // chunk rows each wave loads
     __shared__ double2 nbuf[2][C][64];
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
@@ -1859,7 +1860,7 @@ __global__ __launch_bounds__(256) void ypass_tlds_kernel(SweepArgs a, int nrowbl
     const int s = tile / nrowblk;
     int rb = tile - s * nrowblk;
     if (a.heavy_first) rb = nrowblk - 1 - rb;
-    const int Ny = a.Ny, RB = 4 * R, j0 = rb * RB;
+    const int Ny = a.Ny, RB = NW * R, j0 = rb * RB;
     const int *nst = a.Ny_st[c] + (size_t)s * Ny;
     int mlo = 1 << 30, mhi = -(1 << 30); // the block's noise rows
     for (int q = 0; q < RB && j0 + q < Ny; ++q) {
@@ -1885,12 +1886,12 @@ __global__ __launch_bounds__(256) void ypass_tlds_kernel(SweepArgs a, int nrowbl
     const int col = s * kStrip + 2 * lane;
     const bool live = col < a.Nz_loc;
     const double *np = a.ry[c] + (size_t)a.Nyp[c] * a.Pz + col; // noise row m at np + m * Pz
-    double2 pre[PD][4];
+    double2 pre[PD][LW];
     auto gload = [&](auto K, int u0) {
         constexpr int k0 = decltype(K)::value;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int m = u0 + w + 4 * k;
+        for (int k = 0; k < LW; ++k) {
+            const int m = u0 + w + NW * k;
             pre[k0][k] = live && m <= mhi ? DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)m * a.Pz), m)
                                           : make_double2(0.0, 0.0);
         }
@@ -1898,7 +1899,7 @@ __global__ __launch_bounds__(256) void ypass_tlds_kernel(SweepArgs a, int nrowbl
     auto lstore = [&](auto K, int buf) {
         constexpr int k0 = decltype(K)::value;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) nbuf[buf][w + 4 * k][lane] = pre[k0][k];
+        for (int k = 0; k < LW; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
     };
     double acc0[R], acc1[R];
 #pragma unroll
@@ -1977,6 +1978,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 {
     if constexpr (TABLE) {
         if (a.ylds && !a.per_cell) {
+            if (a.ylds_nw == 8 && R == 1) { // timing variants: 8 rows per block, chunks of 16 or 32 noise rows
+                const int nrb8 = (a.Ny + 7) / 8;
+                const dim3 g8((unsigned)(((long long)a.nstrips * nrb8 + 7) / 8 * 8), 3);
+                if (a.ylds_ch == 32) hipLaunchKernelGGL((ypass_tlds_kernel<1, 2, 8, 32>), g8, dim3(512), 0, st, a, nrb8);
+                else hipLaunchKernelGGL((ypass_tlds_kernel<1, 2, 8, 16>), g8, dim3(512), 0, st, a, nrb8);
+                return hipGetLastError();
+            }
             const int nrowblk = (a.Ny + 4 * R - 1) / (4 * R);
             const unsigned blocks = (unsigned)(((long long)a.nstrips * nrowblk + 7) / 8 * 8);
             // 4 and 8 rows per wave take one chunk in flight: with 2-3 the compiler puts their arrays in scratch

@@ -137,6 +137,7 @@ struct SweepArgs {
     int zocc;                  // z-pass register budget: 0 the compiler's (6 waves per SIMD), 8 (8 waves, zpass WPE)
     int ydepth;                // table y-pass at 1-2 rows per wave: noise 4 groups of 4 rows ahead (1) or 1-2 (0)
     int ylds;                  // table y-pass with the noise staged in LDS per block of 4R rows (ypass_tlds_kernel)
+    int ylds_nw, ylds_ch;      // its waves per block (4; 8 with one row each) and noise rows per chunk (16; 32)
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

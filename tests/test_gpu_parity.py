@@ -166,7 +166,8 @@ def test_golden_native_grid(mode, tuning):
                                          ("packed", dict(ycoop_order=8)), ("packed", dict(ycoop_map=1)),
                                          ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1)),
                                          ("table", dict(ylds=1)), ("table", dict(ylds=2, rows_per_wave=2)),
-                                         ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3))])
+                                         ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
+                                         ("table", dict(ylds_nw=8)), ("table", dict(ylds_nw=8, ylds_ch=32))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
     # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
@@ -307,7 +308,9 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(handoff_batch=1, graph=1), dict(graph=0, handoff_batch=4), dict(ylds=1, rows_per_wave=1),
                 dict(ylds=2, rows_per_wave=2), dict(ylds=3, rows_per_wave=4), dict(ylds=1, rows_per_wave=8),
                 dict(ylds=2, rows_per_wave=1), dict(ylds=3, rows_per_wave=1), dict(ylds=2, rows_per_wave=8),
-                dict(ylds=1, heavy_first=0), dict(ylds=0, heavy_first=1)]
+                dict(ylds=1, heavy_first=0), dict(ylds=2, rows_per_wave=1, ylds_nw=8),
+                dict(ylds=2, rows_per_wave=1, ylds_nw=8, ylds_ch=32), dict(ylds_nw=4, ylds_ch=16),
+                dict(ylds=0, heavy_first=1)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

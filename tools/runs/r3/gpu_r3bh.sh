@@ -1,0 +1,14 @@
+#!/bin/bash
+# Packed z-pass with a 16-tap body (zunroll 8: 16 coefficient loads in flight per wave): parity, A/B.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+O=$GRAFT_REPO_ROOT/gpurun_out/r3bh
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -p no:cacheprovider tests/test_gpu_parity.py \
+  -k "runtime_tuning or fields_vs_oracle" > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for cfg in c2 native c3; do
+  timeout -k 10 200 python3 tools/ab.py --config $cfg --mode packed --rounds 9 --calls 20 --tune-a zunroll=4 --tune-b zunroll=8 \
+    > $O/ab_$cfg.json || { echo "ab failed"; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/ab_$cfg.json'));print('$cfg', d['A'], d['A_median_ms']['zpass_ms'], d['A_median_ms']['wall_ms'], '|', d['B'], d['B_median_ms']['zpass_ms'], d['B_median_ms']['wall_ms'])"
+done

@@ -1331,12 +1331,14 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
-    if constexpr (TABLE && !PC && YU < 4 && R <= 2) {
+    if constexpr (TABLE && !PC && YU < 4 && R <= 4) {
         // Long chains (table mode takes 1-2 rows per wave where N_y >= 128, the reference's grid: up to 426
         // taps per wave at ~3 waves per SIMD): the wave's serial chain of noise-row loads sets the time, so
         // the noise runs kYD groups of 4 rows ahead in a register ring (16 rows in flight instead of 4-8);
         // the group's coefficient window is a scalar load one group ahead. Same products, same order.
-        constexpr int kYD = 4;
+        // 4 rows per wave (c3-class planes): 2 groups ahead, 105 VGPRs as before; c3 -0.8% per call, c2 +-1%
+        // (profiles/r3/bk)
+        constexpr int kYD = R <= 2 ? 4 : 2;
         constexpr int WN = (R + 3 + 7) / 8 * 8;
         if (a.ydeep && a.ywindow && a.ydepth && Nlo == Nhi && t + 4 * kYD - 1 <= bh) {
             const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]

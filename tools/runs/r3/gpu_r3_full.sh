@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r3full}
 O=$GRAFT_REPO_ROOT/gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider --durations=25 \
   > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -60 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Table mode, one rank of c4 over 8 (and 4): RNG stream at high priority (DFAMD_RNG_PRIO=2) vs default, twice.
+# Table mode, one rank of c4 over 8 (and 4): RNG stream at high priority (DFAMD_RNG_PRIO=2, a timing knob since
+# reverted: profiles/r3/rejected/rng_prio_split) vs default, twice.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r3bm

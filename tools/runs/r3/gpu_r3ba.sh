@@ -1,5 +1,5 @@
 #!/bin/bash
-# ypre 2: the next call's y-pass on its own stream (started by its generation's event), so consecutive
+# ypre 2 (reverted since: profiles/r3/rejected/ypre2; the key now clamps to 1): the next call's y-pass on its own stream (started by its generation's event), so consecutive
 # calls' y-passes run back to back beside the z-passes. Parity, then same-handle A/B ypre 0 vs 2 on the
 # reference's grid and c3/c2 packed (and native table for the record).
 set -o pipefail

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Table z-pass with a 16-tap body (zunroll 8: one wait per 16 taps' coefficients and noise): parity, A/B.
+# (zunroll 8 reverted since: profiles/r3/rejected/zunroll8; the key now clamps to 4) Table z-pass with a 16-tap body (zunroll 8: one wait per 16 taps' coefficients and noise): parity, A/B.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r3bg

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Packed z-pass with a 16-tap body (zunroll 8: 16 coefficient loads in flight per wave): parity, A/B.
+# (zunroll 8 reverted since: profiles/r3/rejected/zunroll8; the key now clamps to 4) Packed z-pass with a 16-tap body (zunroll 8: 16 coefficient loads in flight per wave): parity, A/B.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=$GRAFT_REPO_ROOT/gpurun_out/r3bh

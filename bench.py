@@ -89,9 +89,12 @@ def parse(argv=None):
     p.add_argument("--parity", default="on", choices=["on", "off"],
                    help="after the timed region compare every rank's strip with the unsplit plane (table mode)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "off"])
+    p.add_argument("--cpu-full-cols", type=int, default=0,
+                   help="columns of the reference CPU run (0: the GPU plane's own, i.e. the whole plane)")
+    p.add_argument("--cpu-calls", type=int, default=3)  # c3: ~15 s of reference CPU work (5 s per call)
     p.add_argument("--cpu-cols", type=int, default=512,
-                   help="columns of the CPU sample (same rows and half-width rule as the GPU plane)")
-    p.add_argument("--cpu-calls", type=int, default=16)  # ~13 s of reference CPU work (0.8 s per call)
+                   help="columns of the secondary CPU sample (same rows and rule; 0: none)")
+    p.add_argument("--cpu-sample-calls", type=int, default=6)
     p.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--other-configs", default="auto",
                    help="comma list of further configs timed after the main one, same mode and rule; "
@@ -133,26 +136,102 @@ def launch_command(argv, n, port):
             "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
 
 
-def self_launch(argv, n, cmd=None):
+PROGRESS_ENV = "DFAMD_PROGRESS_DIR"
+LAUNCH_TIMEOUT_S = 1500  # the whole N-rank job; a bare 8-GPU run takes a few minutes (profiles/r4/bench8_emulated)
+
+
+def rank_phase(name, rank=None):
+    """Record this rank's current phase (create, warm-up, timed, parity, same-plane, long-run, ...) in
+    $DFAMD_PROGRESS_DIR/rank<r>.log, one timestamped line per phase, so a launch that hangs or dies says
+    where each rank stopped (the parent prints the files on failure)."""
+    d = os.environ.get(PROGRESS_ENV)
+    if not d:
+        return
+    r = int(os.environ.get("RANK", "0")) if rank is None else rank
+    try:
+        with open(os.path.join(d, f"rank{r}.log"), "a") as fh:
+            fh.write(f"{time.strftime('%H:%M:%S')} {time.monotonic():.3f} {name}\n")
+    except OSError:
+        pass
+
+
+def report_progress(d):
+    """Each rank's last recorded phases (stderr): where a failed or timed-out launch stopped."""
+    try:
+        names = sorted(x for x in os.listdir(d) if x.startswith("rank") and x.endswith(".log"))
+    except OSError:
+        names = []
+    if not names:
+        progress(f"no rank recorded a phase in {d}")
+    for nm in names:
+        lines = open(os.path.join(d, nm)).read().splitlines()
+        progress(f"{nm[:-4]}: last phase '{lines[-1].split(' ', 2)[-1] if lines else '-'}' "
+                 f"({len(lines)} recorded: {', '.join(l.split(' ', 2)[-1] for l in lines[-6:])})")
+
+
+def self_launch(argv, n, cmd=None, timeout_s=None):
     """Run the N-rank bench as a child process (never os.exec*: this process has not touched the GPU
     and must not replace itself), relay its JSON line (the one rank 0 prints) to stdout and everything
-    else to stderr, and return the child's return code (1 if it succeeded without a JSON line)."""
+    else to stderr, and return the child's return code (1 if it succeeded without a JSON line).
+
+    The child gets a wall-clock budget (timeout_s, default $DFAMD_BENCH_TIMEOUT or LAUNCH_TIMEOUT_S): on
+    expiry its whole process group (torchrun and every rank) is terminated, then killed, and the launch
+    returns 124. Every rank records its phases under $DFAMD_PROGRESS_DIR (a fresh directory unless set);
+    on any failure the parent prints each rank's last phase."""
+    import shutil
+    import signal
+    import tempfile
+    import threading
+
     cmd = cmd or launch_command(argv, n, free_port())
-    progress("launching " + " ".join(cmd))
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("DFAMD_BENCH_TIMEOUT", LAUNCH_TIMEOUT_S))
+    own_dir = PROGRESS_ENV not in os.environ
+    pdir = os.environ.get(PROGRESS_ENV) or tempfile.mkdtemp(prefix="dfamd_bench_progress_")
+    env = dict(os.environ, **{PROGRESS_ENV: pdir})
+    progress(f"launching (budget {timeout_s:.0f} s, rank phases in {pdir}): " + " ".join(cmd))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1, env=env, start_new_session=True)
+    expired = threading.Event()
+
+    def expire():
+        expired.set()
+        progress(f"wall-clock budget of {timeout_s:.0f} s exceeded: terminating the ranks")
+        for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 0.0)):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                proc.wait(wait)
+                return
+            except subprocess.TimeoutExpired:
+                pass
+
+    timer = threading.Timer(timeout_s, expire)
+    timer.daemon = True
+    timer.start()
     line_out = None
-    for line in proc.stdout:
-        st = line.strip()
-        if st.startswith("{") and '"metric"' in st:
-            line_out = st
-            print(st, flush=True)
-        else:
-            sys.stderr.write(line)
-            sys.stderr.flush()
-    rc = proc.wait()
-    if rc == 0 and line_out is None:
+    try:
+        for line in proc.stdout:
+            st = line.strip()
+            if st.startswith("{") and '"metric"' in st:
+                line_out = st
+                print(st, flush=True)
+            else:
+                sys.stderr.write(line)
+                sys.stderr.flush()
+        rc = proc.wait()
+    finally:
+        timer.cancel()
+    if expired.is_set():
+        rc = 124
+    elif rc == 0 and line_out is None:
         progress("the launched ranks exited 0 without a JSON line")
         rc = 1
+    if rc != 0:
+        report_progress(pdir)
+    if own_dir and rc == 0:
+        shutil.rmtree(pdir, ignore_errors=True)
     return rc
 
 
@@ -173,21 +252,43 @@ def host_cpu():
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(args, Ny, N_min, N_max):
-    """Reference CPU path on this host: df.cpp built from the reference sources
-    (oracle/_ref/ref_harness, g++ -O2, 1 thread), else the oracle restatement."""
+def ref_time(args, Ny, Nz, N_min, N_max, calls, timeout=1200):
+    """The reference itself (oracle/_ref/ref_harness `time`: df.cpp built from the reference sources with
+    g++ -O2, one thread) on an Ny x Nz plane of the SURVEY 8d rule: construction, then `calls` filter(dt)
+    calls minus the CSV write - the region of the reference's own timer (df.cpp:452-462). None when the
+    harness was not built (the box only has what this container built)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     run_root = os.path.join(ROOT, "oracle", "_ref", "run_root")
-    nz = args.cpu_cols
-    sample = (f"{Ny}x{nz} (the GPU plane's {Ny} rows and N {N_min}-{N_max} rule, {nz} columns), "
+    if not (os.path.exists(exe) and os.path.isdir(run_root)):
+        return None
+    out = subprocess.run([exe, "time", run_root, str(args.seed), str(Ny), str(Nz), str(N_min), str(N_max),
+                          str(args.dt), str(calls)], capture_output=True, text=True, check=True, timeout=timeout)
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline(args, Ny, Nz, N_min, N_max):
+    """Reference CPU path on this host, on the WHOLE plane the GPU line times: df.cpp
+    built from the reference sources (oracle/_ref/ref_harness, g++ -O2, 1 thread), `--cpu-calls` calls
+    (c3: ~5 s each after a ~1 min construction holding 21 GB of host coefficients); else the oracle
+    restatement. A narrower sample (`--cpu-cols` columns, same rows and rule) is timed beside it, and the
+    sample/whole ratio of cells/s is the measured check of the per-cell extrapolation to c4/c5."""
+    nz = Nz if args.cpu_full_cols <= 0 else args.cpu_full_cols
+    sample = (f"the whole {Ny}x{nz} plane (the GPU line's rows, columns and N {N_min}-{N_max} rule), "
               f"{args.cpu_calls} filter(dt) calls after construction")
-    if os.path.exists(exe) and os.path.isdir(run_root):
-        out = subprocess.run([exe, "time", run_root, str(args.seed), str(Ny), str(nz), str(N_min), str(N_max),
-                              str(args.dt), str(args.cpu_calls)], capture_output=True, text=True, check=True)
-        rec = json.loads(out.stdout.strip().splitlines()[-1])
+    rec = ref_time(args, Ny, nz, N_min, N_max, args.cpu_calls)
+    if rec is not None:
         res = {"value": Ny * nz / rec["mean_s"], "unit": "cells/s", "cores": 1, "kind": "reference",
-               "sample": sample, "s_per_call": rec["mean_s"],
+               "sample": sample, "s_per_call": rec["mean_s"], "best_s_per_call": rec["best_s"],
+               "construction_s": rec["setup_s"],
                "stage_s": {k: rec[k] for k in ("noise_s", "sweeps_s", "correlate_s", "rst_s", "sra_s")}}
+        if args.cpu_cols > 0 and args.cpu_cols < nz:
+            sm = ref_time(args, Ny, args.cpu_cols, N_min, N_max, args.cpu_sample_calls)
+            sm_rate = Ny * args.cpu_cols / sm["mean_s"]
+            res["column_sample"] = {
+                "sample": f"{Ny}x{args.cpu_cols}, {args.cpu_sample_calls} calls", "value": round(sm_rate, 1),
+                "s_per_call": sm["mean_s"], "sample_over_whole": round(sm_rate / res["value"], 4),
+                "note": "cells/s of a narrower plane of the same rows and rule over the whole plane's: "
+                        "1.0 means the per-cell cost is column-independent (the c4/c5 extrapolation's premise)"}
     else:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
@@ -199,11 +300,11 @@ def cpu_baseline(args, Ny, N_min, N_max):
         res = {"value": Ny * nz / dt, "unit": "cells/s", "cores": 1, "kind": "port", "sample": sample,
                "s_per_call": dt}
     res.update(host_cpu())
-    # BASELINE.md CPU plan step 5: the multi-GPU configs per cell from this sample (derived, not run)
+    # BASELINE.md CPU plan step 5: the multi-GPU configs per cell from this plane (derived, not run)
     res["extrapolated"] = {
         name: {"cells": CONFIGS[name][1] * CONFIGS[name][2],
                "s_per_call": round(CONFIGS[name][1] * CONFIGS[name][2] / res["value"], 3),
-               "derived": "cells / the sample's cells/s (per-cell cost is column-independent; same N rule)"}
+               "derived": "cells / the whole plane's cells/s (same N rule; column_sample checks the per-cell premise)"}
         for name in ("c4", "c5")}
     return res
 
@@ -234,11 +335,11 @@ def cpu_baseline_parallel(args, Ny, N_min, N_max):
     env = dict(os.environ, ORACLE_LIB=lib, OMP_NUM_THREADS=str(threads))
     nz = args.cpu_cols
     out = subprocess.run([sys.executable, "-c", PAR_SCRIPT, os.path.join(ROOT, "oracle"), str(Ny), str(nz),
-                          str(N_min), str(N_max), str(args.seed), str(args.dt), str(args.cpu_calls)],
+                          str(N_min), str(N_max), str(args.seed), str(args.dt), str(args.cpu_sample_calls)],
                          env=env, capture_output=True, text=True, check=True, timeout=600)
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     return {"value": Ny * nz / rec["s_per_call"], "unit": "cells/s", "cores": threads, "kind": "port",
-            "sample": f"{Ny}x{nz} (as cpu_baseline), {args.cpu_calls} filter(dt) calls",
+            "sample": f"{Ny}x{nz} (cpu_baseline's column sample), {args.cpu_sample_calls} filter(dt) calls",
             "s_per_call": rec["s_per_call"],
             "note": "oracle restatement with OpenMP over the rows of the sweeps and elementwise steps "
                     "(RNG serial); not the reference, which is single-threaded"}
@@ -332,13 +433,14 @@ def make_filter(dfamd, ctx, wl, args, coeff_mode, split=True, comm_id=None):
     return dfamd.DigitalFilter(**kw)
 
 
-def timed(ctx, h, args, min_warm_s=0.0, profile=True, collective=True):
+def timed(ctx, h, args, min_warm_s=0.0, profile=True, collective=True, label=""):
     """W untimed calls, then exactly K calls between barrier + synchronize; hipEvent phase profile.
     min_warm_s > 0 (secondary lines only: alt mode, other configs) keeps warming up until that much
     time has passed: a 0.4 ms table-mode call otherwise starts timing while the clocks still ramp
     (c3 table: 0.395 ms/call after 5 calls, 0.370 after 140; profiles/r2/table_warmup.txt)."""
     torch = ctx.torch
     calls = 0
+    rank_phase(f"{label}: warm-up ({args.warmup} calls)")
     for _ in range(args.warmup):
         h.filter(args.dt)
         calls += 1
@@ -351,6 +453,7 @@ def timed(ctx, h, args, min_warm_s=0.0, profile=True, collective=True):
             calls += 1
         h.sync()
     h.set_profiling(profile, every=args.profile_every if args.steps >= 2 * args.profile_every else 1)
+    rank_phase(f"{label}: timed ({args.steps} calls)")
     if collective:
         ctx.barrier()
     torch.cuda.synchronize()
@@ -391,6 +494,7 @@ def parity_check(dfamd, ctx, wl, args, h, calls, ref=None):
     """This rank's strip after construction + `calls` filter(dt) calls against the whole plane run unsplit in table mode
     on this rank's own GPU (packed and table mode, any strip count: bit-identical by construction)."""
     own = ref is None
+    rank_phase(f"{wl['name']}: parity (whole plane unsplit, table mode)")
     if own:
         ref = make_filter(dfamd, ctx, wl, args, "table", split=False)
         for _ in range(calls):
@@ -434,10 +538,11 @@ def roofline_of(h, prof, args, config_name):
 
 def run_config(dfamd, ctx, wl, args, comm_id, min_warm_s=0.0):
     """Create and time one workload on every rank; returns the handle and this rank's record."""
+    rank_phase(f"{wl['name']}: create (df_create, step 0)")
     t_setup = time.perf_counter()
     f = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
     t_setup = time.perf_counter() - t_setup
-    elapsed, prof, ncalls = timed(ctx, f, args, min_warm_s)
+    elapsed, prof, ncalls = timed(ctx, f, args, min_warm_s, label=wl["name"])
     f.calls_done = ncalls  # filter(dt) calls after step 0, for the parity reference
     rank_rec = {"rank": ctx.rank, "elapsed_s": elapsed, "phase_ms_per_call": per_call(prof),
                 "roofline": roofline_of(f, prof, args, wl["name"]), "columns": [f.z0, f.z1],
@@ -451,6 +556,7 @@ def same_plane_1gpu(dfamd, ctx, wl, args, split_ms):
     closed its strip: the 1-GPU time of the SAME plane the N ranks split, and the speedup over it.
     The other ranks wait at the barrier. (near-linear vs 1 GPU on one plane.)"""
     res = None
+    rank_phase(f"{wl['name']}: same-plane baseline ({'timing' if ctx.rank == 0 else 'waiting at the barrier'})")
     if ctx.rank == 0:
         progress(f"{wl['name']}: whole plane on one GPU (same-plane baseline)")
         h = make_filter(dfamd, ctx, wl, args, args.coeff_mode, split=False)
@@ -474,6 +580,7 @@ def long_run(dfamd, ctx, wl, args, steps, comm_id):
     end, SURVEY 4's invariant over the whole plane: per row, the mean of u'^2, v'^2, w'^2 over time
     and every rank's columns against R11, R22, R33 (rows with R11 > 1% of its max)."""
     torch = ctx.torch
+    rank_phase(f"{wl['name']}: long run ({steps} calls)")
     h = make_filter(dfamd, ctx, wl, args, args.coeff_mode, comm_id=comm_id)
     h.filter(args.dt)
     h.sync()
@@ -562,6 +669,7 @@ def main(argv=None):
         return self_launch(argv, args.gpus)
     ctx = Ctx()
     if args.dry_run:  # tests/test_bench_launch.py: the self-launch reaches N ranks with the right env
+        rank_phase("dry-run", ctx.rank)
         if ctx.rank == 0:
             print(json.dumps({"metric": "dry-run", "n_gpus": ctx.world, "gpus_arg": args.gpus,
                               "master_addr": os.environ.get("MASTER_ADDR"), "argv": argv}), flush=True)
@@ -572,9 +680,10 @@ def main(argv=None):
     wl = plan_workload(name, ctx.world, args.scaling)
     others_arg = args.other_configs
     if others_arg == "auto":
-        others_arg = "native,c2" if ctx.world == 1 else "c5"
+        others_arg = "native,c2,c1" if ctx.world == 1 else "c5"
 
     # torch first: libdfamd.so then binds to the same HIP runtime torch loaded.
+    rank_phase("init: torch + process group", ctx.rank)
     import torch
     ctx.init(torch)
     sys.path.insert(0, PKG)
@@ -675,17 +784,31 @@ def main(argv=None):
             others[oname]["parity"] = [p for p in ops if not p["ok"]]
         if ctx.world > 1 and args.same_plane == "auto":
             others[oname]["same_plane_1gpu"] = same_plane_1gpu(dfamd, ctx, owl, args, osum["ms_per_step"])
+        if oname == "c1" and ctx.world == 1 and ctx.rank == 0 and args.cpu_baseline == "auto":
+            # BASELINE configs[0], the reference's CPU-runnable case: the reference itself on one core beside
+            # the GPU's c1 line (test/cpp-main.cpp:12-17 builds this object; df.cpp:452-464 is its timer)
+            try:
+                rr = ref_time(args, owl["Ny"], owl["Nz"], owl["N_min"], owl["N_max"], 400, timeout=300)
+                if rr is not None:
+                    cells = owl["Ny"] * owl["Nz"]
+                    others[oname]["cpu_reference"] = {
+                        "value": round(cells / rr["mean_s"], 1), "unit": "cells/s", "cores": 1, "kind": "reference",
+                        "ms_per_call": round(rr["mean_s"] * 1e3, 4), "calls": 400,
+                        "gpu_over_cpu": round(osum["value"] / (cells / rr["mean_s"]), 1)}
+            except Exception as e:
+                others[oname]["cpu_reference"] = {"error": str(e)[-300:]}
         if oname == "c5" and ctx.world > 1 and args.long_run == "auto":
             others[oname]["long_run"] = long_run(dfamd, ctx, owl, args, 10000, ctx.comm_id(dfamd))
 
     dropin = None
+    rank_phase("reports (drop-in, CPU baseline, JSON line)")
     if ctx.rank == 0 and ctx.world == 1 and args.dropin == "auto":
         dropin = dropin_timing(args)
     if ctx.rank == 0:
         cpu = cpu_par = None
         if args.cpu_baseline == "auto" and ctx.world == 1 and wl["plane"] != "native":
             try:
-                cpu = cpu_baseline(args, wl["Ny"], wl["N_min"], wl["N_max"])
+                cpu = cpu_baseline(args, wl["Ny"], wl["Nz"], wl["N_min"], wl["N_max"])
             except Exception as e:  # reported, never fatal for the GPU number
                 cpu = {"error": str(e)}
             try:
@@ -739,8 +862,13 @@ def main(argv=None):
     ctx.barrier()
     if ctx.dist is not None:
         ctx.dist.destroy_process_group()
+    rank_phase("done")
     return 0
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    try:
+        sys.exit(main())
+    except Exception as e:  # the rank's last phase names the failure for the launching parent
+        rank_phase(f"failed: {type(e).__name__}: {str(e)[:200]}")
+        raise

@@ -79,6 +79,7 @@ struct PhaseEvents {
                      // prefetched y-pass's start and end (ypre)
     bool rng = false;
     bool ypre = false;
+    int gens = 0; // generations enqueued during the call: e[4] before the first, e[5] after the last
 };
 
 } // namespace
@@ -215,6 +216,8 @@ struct df_handle {
     std::vector<PhaseEvents> ev;
     size_t ev_used = 0;
     df_profile prof{};
+    double prof_rng_span = 0; // RNG stream time of the profiled calls' generation bursts (ms)
+    long long prof_rng_gens = 0; // generations in those bursts
     std::vector<void *> allocs;
 };
 
@@ -419,9 +422,12 @@ int drain_profile(df_handle *h)
         float t[3] = {0, 0, 0}, tot = 0, r = 0;
         for (int p = 0; p < 3; ++p) (void)hipEventElapsedTime(&t[p], h->ev[i].e[p], h->ev[i].e[p + 1]);
         (void)hipEventElapsedTime(&tot, h->ev[i].e[0], h->ev[i].e[3]);
-        if (h->ev[i].rng) (void)hipEventElapsedTime(&r, h->ev[i].e[4], h->ev[i].e[5]);
+        if (h->ev[i].rng) {
+            (void)hipEventElapsedTime(&r, h->ev[i].e[4], h->ev[i].e[5]);
+            h->prof_rng_span += r;
+            h->prof_rng_gens += h->ev[i].gens;
+        }
         if (h->ev[i].ypre) (void)hipEventElapsedTime(&t[0], h->ev[i].e[6], h->ev[i].e[7]); // on rng_stream
-        h->prof.rng_ms += r;
         h->prof.ypass_ms += t[0];
         h->prof.halo_ms += t[1];
         h->prof.zpass_ms += t[2];
@@ -429,8 +435,13 @@ int drain_profile(df_handle *h)
         h->prof.calls++;
         h->ev[i].rng = false;
         h->ev[i].ypre = false;
+        h->ev[i].gens = 0;
     }
     h->ev_used = 0;
+    // Every call consumes one generation, but with hand-off batches (hb > 1) a call enqueues a burst of hb
+    // generations at an epoch start and none mid-epoch, and sampled profiling may always land on the same
+    // epoch position: rng_ms is therefore the measured time per generation times the calls profiled.
+    h->prof.rng_ms = h->prof_rng_gens ? h->prof_rng_span / (double)h->prof_rng_gens * (double)h->prof.calls : 0.0;
     return DF_OK;
 }
 
@@ -468,7 +479,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
     }
-    if (prof_on(h)) {
+    if (prof_on(h) && h->ev[h->ev_used].gens++ == 0) { // a burst of hb generations is timed as one span
         ev_record(h, 4);
         h->ev[h->ev_used].rng = true;
     }
@@ -746,13 +757,20 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
     ev_record(h, 2); // halo_ms is the pack alone here; the exchange runs under zpass_ms
     HIP_OR(hipStreamWaitEvent(h->comm_stream, h->ev_packed, 0), DF_EHIP);
-    if (peer && (rc = halo_sendrecv(h, h->comm_stream))) return rc;
-    if (peer && (rc = phase_halo_unpack(h, h->comm_stream))) return rc;
-    if ((rc = phase_zpass(h, corr, sra, dt, 2, h->comm_stream))) return rc; // edge strips
-    HIP_OR(hipEventRecord(h->ev_unpacked, h->comm_stream), DF_EHIP);
-    if ((rc = phase_zpass(h, corr, sra, dt, 1))) return rc; // interior strips
-    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_unpacked, 0), DF_EHIP);
-    return DF_OK;
+    // From here on comm_stream holds work that reads the send buffers: whatever fails below, the stream
+    // joins comm_stream before returning, so the next call's pack cannot overwrite buffers still in flight.
+    auto join = [h](int code) {
+        if (hipEventRecord(h->ev_unpacked, h->comm_stream) == hipSuccess)
+            (void)hipStreamWaitEvent(h->stream, h->ev_unpacked, 0);
+        else
+            (void)hipStreamSynchronize(h->comm_stream);
+        return code;
+    };
+    if (peer && (rc = halo_sendrecv(h, h->comm_stream))) return join(rc);
+    if (peer && (rc = phase_halo_unpack(h, h->comm_stream))) return join(rc);
+    if ((rc = phase_zpass(h, corr, sra, dt, 2, h->comm_stream))) return join(rc); // edge strips
+    rc = phase_zpass(h, corr, sra, dt, 1); // interior strips
+    return join(rc);
 }
 
 // part 0: every strip; 1: the halo-interior strips; 2: the edge strips around them (halo_interior)
@@ -1533,13 +1551,16 @@ int step0(df_handle *h)
 void destroy(df_handle *h)
 {
     if (!h) return;
+    // Drain every stream before any buffer or communicator goes: comm_stream may still hold a send/recv,
+    // an unpack or the edge z-pass when a call failed part-way (phase_halo_zpass's error returns).
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
+    if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
     for (void *p : h->allocs) {
+        registry_release(p); // before the free: another thread's hipMalloc may get the address back at once
         (void)hipFree(p);
-        registry_release(p);
     }
     if (h->err_host) (void)hipHostFree(h->err_host);
     if (h->rng_comm) ncclCommDestroy(h->rng_comm);
@@ -1555,7 +1576,7 @@ void destroy(df_handle *h)
         if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
     }
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
-    if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream), (void)hipStreamDestroy(h->comm_stream);
+    if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
     if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
     if (h->ev_unpacked) (void)hipEventDestroy(h->ev_unpacked);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -2301,6 +2322,8 @@ int df_set_profiling(df_handle *h, int on)
     h->profile_every = on > 1 ? on : 1;
     h->prof_seq = 0;
     h->prof = df_profile{};
+    h->prof_rng_span = 0;
+    h->prof_rng_gens = 0;
     return rc;
 }
 

@@ -61,3 +61,37 @@ def test_bare_bench_propagates_a_failing_rank():
                        cwd=ROOT)
     assert r.returncode != 0
     assert r.stdout.strip() == ""
+
+
+def test_self_launch_budget_kills_the_ranks_and_reports_their_phase(capsys, tmp_path):
+    # a rank stuck (here: asleep) must not hold the launch past its budget; the whole
+    # process group goes, the parent returns 124 and prints where each rank stopped
+    import time
+    child = ("import os, time; d = os.environ['DFAMD_PROGRESS_DIR']; "
+             "open(os.path.join(d, 'rank0.log'), 'a').write('00:00:00 0.0 c4: timed (50 calls)\\n'); "
+             "open(os.path.join(d, 'rank1.log'), 'a').write('00:00:00 0.0 c4: create (df_create, step 0)\\n'); "
+             "time.sleep(120)")
+    env_before = os.environ.pop(bench.PROGRESS_ENV, None)
+    t0 = time.monotonic()
+    try:
+        rc = bench.self_launch([], 2, cmd=[sys.executable, "-c", child], timeout_s=3)
+    finally:
+        if env_before is not None:
+            os.environ[bench.PROGRESS_ENV] = env_before
+    took = time.monotonic() - t0
+    err = capsys.readouterr().err
+    assert rc == 124
+    assert took < 30, took
+    assert "budget of 3 s exceeded" in err
+    assert "rank0: last phase 'c4: timed (50 calls)'" in err
+    assert "rank1: last phase 'c4: create (df_create, step 0)'" in err
+
+
+def test_bare_bench_ranks_record_their_phases(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=dict(_env(), DFAMD_PROGRESS_DIR=str(tmp_path)),
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for rank in (0, 1):
+        lines = (tmp_path / f"rank{rank}.log").read_text().splitlines()
+        assert lines and lines[-1].endswith("dry-run"), lines

@@ -105,3 +105,18 @@ def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
     outs = run_world(world, mode, replicate, Nz=Nz, N_min=4, N_max=64, emulate=True,
                      extra=dict(halo_overlap=overlap))
     check_world(outs, world, replicate, Nz=Nz)
+
+
+@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 0)])
+def test_rccl_c4_real_partition_emulated(mode, replicate):
+    """The partition the driver's 8-GPU bench runs first: BASELINE configs[3] (c4,
+    2048 x 8192, N 4-64) in eight 2048 x 1024 strips, each rank's 3.1 MB halos per side through the
+    product's grouped ncclSend/ncclRecv (RCCL socket transport between emulated hosts on one GPU), every
+    strip bit-equal to the whole plane run unsplit after step 0 and two calls."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(8, mode, replicate, Ny=2048, Nz=8192, N_min=4, N_max=64, dts=(1e-8, 1e-5), emulate=True)
+    check_world(outs, 8, replicate, Nz=8192)
+    assert sorted(o["columns"] for o in outs) == [[r * 1024, (r + 1) * 1024] for r in range(8)]
+    for o in outs:
+        assert o["comm"]["halo_bytes_sent"] == o["comm"]["halo_peers"] * 2048 * 64 * 3 * 8, o["comm"]

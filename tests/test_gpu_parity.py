@@ -4,9 +4,11 @@ reference's golden vectors.
 Bar (SURVEY 8c / BASELINE north_star):
   * pcg32 stream position, polar accept decisions and the cached normal:
     bit-exact (checked through the stream state after every call);
-  * fields u', v', w', T', rho': |a - b| <= 1e-6 * max(|b|, RMS_row(b)) per cell
-    (TOL below). The sweeps themselves are bit-exact given equal noise; the only
-    admitted difference is the device log() in the polar transform (<= 1 ulp).
+  * fields u', v', w', T', rho': bit-identical to the oracle and to the reference's
+    own fixtures (np.array_equal) on every plane kind: synthetic, the reference's grid,
+    per-cell half-widths on real grids, z-strips. SURVEY 8c's looser bar
+    (|a - b| <= 1e-6 * max(|b|, RMS_row(b)), TOL below) is kept only for the
+    fast_log 0/1 noise variants, whose log is not glibc's.
 """
 import os
 
@@ -40,6 +42,21 @@ def assert_fields(gpu, ref, tol=TOL, what=""):
         worst[k] = e
         assert e <= tol, f"{what} field {k}: rel err {e:.3e} > {tol}"
     return worst
+
+
+def assert_same(a, b, what=""):
+    """Bit-identity with the first differing cell named."""
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if not np.array_equal(a, b):
+        bad = np.argwhere(a != b)
+        i = tuple(int(x) for x in bad[0])
+        raise AssertionError(f"{what}: {len(bad)} cells differ; first at {i}: {a[i]!r} vs {b[i]!r}")
+
+
+def assert_stats(a, ref, what=""):
+    st3 = np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
+    assert np.allclose(st3, ref, rtol=1e-12, atol=1e-300), (what, st3, ref)
 
 
 def oracle_synth(Ny, Nz, N_min, N_max, seed=None, rng=None):
@@ -122,13 +139,10 @@ def check_golden_case(name, coeff_mode="packed", rows_per_wave=8):
         got = f.fields()
         for k in FIELDS:
             a = got[k]
-            ref_rows = g[f"s{s}_{k}_rows"]
-            assert float(rel_err(a[rows], ref_rows).max()) <= TOL, (name, s, k)
-            st3 = np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
-            ref = g[f"s{s}_{k}_stats"]
-            assert np.allclose(st3, ref, rtol=1e-9, atol=1e-300), (name, s, k, st3, ref)
+            assert_same(a[rows], g[f"s{s}_{k}_rows"], f"{name} step {s} {k} rows")
+            assert_stats(a, g[f"s{s}_{k}_stats"], (name, s, k))
             if s in full:
-                assert float(rel_err(a, g[f"s{s}_{k}"]).max()) <= TOL, (name, s, k)
+                assert_same(a, g[f"s{s}_{k}"], f"{name} step {s} {k}")
     return f
 
 
@@ -156,10 +170,8 @@ def test_golden_native_grid(mode, tuning):
             f.filter(float(g["dt"]))
         got = f.fields()
         for k in FIELDS:
-            assert float(rel_err(got[k][rows], g[f"s{s}_{k}_rows"]).max()) <= TOL, (s, k)
-            a = got[k]
-            st3 = np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
-            assert np.allclose(st3, g[f"s{s}_{k}_stats"], rtol=1e-9, atol=1e-300), (s, k)
+            assert_same(got[k][rows], g[f"s{s}_{k}_rows"], f"native step {s} {k} rows")
+            assert_stats(got[k], g[f"s{s}_{k}_stats"], (s, k))
 
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=8)), ("packed", dict(ycoop_order=1)),
@@ -191,11 +203,15 @@ def test_native_grid_bitexact_vs_oracle(mode, tuning):
 def test_fields_vs_oracle(spec):
     o = oracle_synth(*spec, seed=3)
     g = gpu_synth(*spec, seed=3)
-    assert_fields(g.fields(), o.fields(), what="step0")
+    gf, of = g.fields(), o.fields()
+    for k in FIELDS:
+        assert_same(gf[k], of[k], f"step0 {k}")
     for dt in (1e-8, 1e-8, 1e-5):
         o.filter(dt)
         g.filter(dt)
-        assert_fields(g.fields(), o.fields(), what=f"dt={dt}")
+        gf, of = g.fields(), o.fields()
+        for k in FIELDS:
+            assert_same(gf[k], of[k], f"dt={dt} {k}")
     for c in range(3):
         assert np.array_equal(g.field(f"filt_old_{'uvw'[c]}").shape, (o.Ny, o.Nz))
 
@@ -244,8 +260,9 @@ def test_c2_512_variable_halfwidth_vs_oracle():
         o.filter(dt)
         g.filter(dt)
     assert g.rng_state() == o.rng.state
-    w = assert_fields(g.fields(), o.fields(), what="c2")
-    print("c2 worst rel err", w)
+    gf, of = g.fields(), o.fields()
+    for k in FIELDS:
+        assert_same(gf[k], of[k], f"c2 {k}")
 
 
 # ------------------------------------------------------- variants are identical
@@ -663,10 +680,10 @@ def test_golden_grid_plane_per_cell_halfwidths(mode, rpw, tuning):
             assert f.rng_state() == o.rng.state
         for k in FIELDS:
             a = f.field(k)
-            st3 = np.array([a.sum(), (a * a).sum(), np.abs(a).max()])
-            assert np.allclose(st3, g[f"s{s}_{k}_stats"], rtol=1e-9, atol=1e-300), (s, k)
-            if s in full:
-                assert float(rel_err(a, g[f"s{s}_{k}"]).max()) <= TOL, (s, k)
+            assert_stats(a, g[f"s{s}_{k}_stats"], (s, k))
+            if s in full:  # the reference's own fields on its per-cell N: bit for bit
+                assert_same(a, g[f"s{s}_{k}"], f"grid_s3 step {s} {k}")
+            assert_same(a, o.field(k), f"grid_s3 vs oracle step {s} {k}")
 
 
 @pytest.mark.parametrize("mode", ["packed", "table"])
@@ -682,7 +699,7 @@ def test_grid_plane_vs_oracle_three_strips(mode):
             o.filter(dt)
         assert f.rng_state() == o.rng.state
         for k in FIELDS:
-            assert float(rel_err(f.field(k), o.field(k)).max()) <= TOL, (dt, k)
+            assert_same(f.field(k), o.field(k), f"grid 3 strips dt={dt} {k}")
 
 
 def test_grid_plane_table_equals_packed_and_strips_equal_whole():
@@ -790,7 +807,7 @@ def test_random_planes_vs_oracle(case):
         assert all(h.rng_state() == o.rng.state for h in hs)
         for k in FIELDS:
             got = np.concatenate([h.field(k) for h in hs], axis=1)
-            assert float(rel_err(got, o.field(k)).max()) <= TOL, (dt, k)
+            assert_same(got, o.field(k), f"dt={dt} {k}")
 
 
 def test_handles_driven_from_two_host_threads():

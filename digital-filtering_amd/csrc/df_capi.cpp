@@ -155,6 +155,7 @@ struct df_handle {
     long long *part = nullptr; // K2a run totals -> run prefixes (K2b)
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
     int *wave_counts = nullptr; // accepted attempts per wave of each block (K1 -> K2c)
+    uint8_t *gcount = nullptr;  // accepted attempts per 64-attempt group (K1 -> K2g/K2l/K3r, gen_dense 2)
     WaveTask *tasks = nullptr;  // waves K3 runs (K2c)
     int *ntasks = nullptr;
     int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped, [2] halo loopback mismatches
@@ -163,6 +164,14 @@ struct df_handle {
     int rng_chunk = 0;        // blocks counted by each z-strip rank (split counting, SURVEY 8e option A)
     bool split_count = false;
     ncclComm_t rng_comm = nullptr;           // second communicator: the count all-gather runs on rng_stream
+    // Fused exchange (round 4; split counting with the run generation): the next generation's K1 goes on
+    // rng_stream at the start of a call and its group counts travel inside the call's halo group - one grouped
+    // RCCL operation per df_filter (north star) - and the rest of that generation runs after the group, beside
+    // the z-pass. gen_pending: K1 enqueued, the exchange and gen_end not yet.
+    int fused_x = 1;
+    bool gen_pending = false;
+    RngGeom pend_g{};
+    hipEvent_t ev_xchg = nullptr; // DFAMD_SOLO_STRIP: where the halo group would sit (after the pack)
     hipEvent_t ev_counted = nullptr;         // in-process groups: this handle's counts are ready
     hipEvent_t ev_halo = nullptr;            // split counting: the halo of the call just enqueued is done
     // RCCL z-strips (round 3): the halo send/recv, the unpack and the edge strips' z-pass run on comm_stream
@@ -473,7 +482,8 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
-    g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? 1 : 0;
+    g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? h->gen_dense : 0;
+    g.gcount = g.gen_dense == 2 ? h->gcount : nullptr; // K1 writes the group counts the run form scans
     if (!h->k3a_fast) g.chunk_dest[0] = g.chunk_dest[1] = nullptr;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
@@ -564,6 +574,10 @@ int launch_gen_group(std::vector<df_handle *> &hs)
             HIP_OR(hipMemcpyAsync(h->wave_counts + at * kWavesPerBlock, hs[o]->wave_counts + at * kWavesPerBlock,
                                   (size_t)h->rng_chunk * kWavesPerBlock * sizeof(int), hipMemcpyDefault, rss[r]),
                    DF_EHIP);
+            if (gs[r].gen_dense == 2)
+                HIP_OR(hipMemcpyAsync(h->gcount + at * 64, hs[o]->gcount + at * 64, (size_t)h->rng_chunk * 64,
+                                      hipMemcpyDefault, rss[r]),
+                       DF_EHIP);
         }
         if ((rc = gen_end(h, gs[r], rss[r]))) return rc;
     }
@@ -585,15 +599,23 @@ int launch_gen(df_handle *h)
         int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
         const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
+        const size_t ngc = (size_t)h->rng_chunk * 64;
+        uint8_t *gmine = h->gcount + (size_t)h->rank * ngc;
         if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
             // Never concurrent with the halo send/recv of the other communicator: every rank issues
             // the all-gather only after its own halo group of the call just enqueued has completed,
             // so the two communicators' kernels run in the same order on every rank.
             if (h->ev_halo) HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
             NCCL_OR(ncclGroupStart());
-            NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
-            NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
+            if (g.gen_dense == 2) { // run form: the group counts alone (block counts are their sums)
+                NCCL_OR(ncclAllGather(gmine, h->gcount, ngc, ncclUint8, h->rng_comm, rs));
+            } else {
+                NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
+                NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
+            }
             NCCL_OR(ncclGroupEnd());
+        } else if (g.gen_dense == 2) { // DFAMD_SOLO_STRIP: this rank's group counts stand in for every share
+            HIP_OR(launch_replicate_share(h->gcount, ngc, h->world, h->rank, rs), DF_EHIP);
         } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
             for (int o = 0; o < h->world; ++o)
                 if (o != h->rank) {
@@ -631,8 +653,10 @@ int consume_gen(df_handle *h)
 // hb_burst 1 enqueues a whole epoch at its predecessor's first step instead (one burst of hb
 // generations); spread (the default) enqueues one per step, so the last generation of epoch e + 1 goes
 // under the last step of epoch e, just before epoch e + 1 waits for it.
+int fused_gen_end(df_handle *h);
 int prefetch_gen(df_handle *h)
 {
+    if (int rc = fused_gen_end(h)) return rc;
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
     long long need = h->gen_used + h->hb;
@@ -644,6 +668,44 @@ int prefetch_gen(df_handle *h)
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
     return DF_OK;
+}
+
+// The fused exchange applies to split-counting z-strip handles of one process per GPU (RCCL, or the solo-strip
+// timing stand-in) with the run generation and one generation per hand-off.
+bool fused_active(const df_handle *h)
+{
+    return h->fused_x && h->split_count && h->world > 1 && (h->comm || h->solo_strip) && !h->group && h->overlap &&
+           h->hb == 1 && h->gen_dense == 2 && h->geom.cstate;
+}
+
+// Start of a visible step: the next generation's K1 (its group counts) on rng_stream, ev_counted after it.
+int fused_gen_begin(df_handle *h)
+{
+    h->gen_pending = false; // a K1 left pending by a failed call is simply redone
+    if (!fused_active(h) || h->gen_launched != h->gen_used) return DF_OK;
+    hipStream_t rs;
+    int rc = gen_begin(h, h->pend_g, rs);
+    if (rc) return rc;
+    if (h->pend_g.gen_dense != 2) return DF_OK; // cannot happen with fused_active; the plain path then runs
+    HIP_OR(hipEventRecord(h->ev_counted, rs), DF_EHIP);
+    h->gen_pending = true;
+    return DF_OK;
+}
+
+// After the halo group (which carried the group counts): scan, locate, generate on rng_stream.
+int fused_gen_end(df_handle *h)
+{
+    if (!h->gen_pending) return DF_OK;
+    h->gen_pending = false;
+    hipStream_t rs = h->rng_stream;
+    if (h->comm) {
+        HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
+    } else { // solo strip: the same dependency on this call's halo position, the exchange by a stand-in copy
+        HIP_OR(hipStreamWaitEvent(rs, h->ev_xchg, 0), DF_EHIP);
+        const size_t ngc = (size_t)h->rng_chunk * 64;
+        HIP_OR(launch_replicate_share(h->gcount, ngc, h->world, h->rank, rs), DF_EHIP);
+    }
+    return gen_end(h, h->pend_g, rs);
 }
 
 int phase_ypass(df_handle *h, int comps_mask)
@@ -697,7 +759,12 @@ int halo_loopback(df_handle *h)
 // The grouped send/recv with rank +- 1 on stream st, then ev_halo there.
 int halo_sendrecv(df_handle *h, hipStream_t st)
 {
+    if (h->gen_pending) HIP_OR(hipStreamWaitEvent(st, h->ev_counted, 0), DF_EHIP); // the next generation's counts
     NCCL_OR(ncclGroupStart());
+    if (h->gen_pending) { // fused exchange: the next generation's group counts, in place, in the same group
+        const size_t ngc = (size_t)h->rng_chunk * 64;
+        NCCL_OR(ncclAllGather(h->gcount + (size_t)h->rank * ngc, h->gcount, ngc, ncclUint8, h->comm, st));
+    }
     if (h->rank > 0) {
         NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
         NCCL_OR(ncclRecv(h->recv_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
@@ -714,7 +781,11 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
 int phase_halo_rccl(df_handle *h)
 {
     if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
-    if (h->solo_strip) return phase_halo_pack(h); // timing only: the pack, no exchange
+    if (h->solo_strip) { // timing only: the pack, no exchange
+        int rc = phase_halo_pack(h);
+        if (!rc && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->stream), DF_EHIP);
+        return rc;
+    }
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
     int rc = phase_halo_pack(h);
     if (rc || (rc = halo_sendrecv(h, h->stream))) return rc;
@@ -755,6 +826,7 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     }
     if ((rc = phase_halo_pack(h))) return rc;
     HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
+    if (!peer && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->stream), DF_EHIP);
     ev_record(h, 2); // halo_ms is the pack alone here; the exchange runs under zpass_ms
     HIP_OR(hipStreamWaitEvent(h->comm_stream, h->ev_packed, 0), DF_EHIP);
     // From here on comm_stream holds work that reads the send buffers: whatever fails below, the stream
@@ -1337,6 +1409,8 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
     if ((rc = dalloc_t(h, &h->part, (nb_pad + 1023) / 1024))) return rc;
     if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
     if ((rc = dalloc_t(h, &h->wave_counts, (size_t)nb_pad * kWavesPerBlock))) return rc;
+    if ((rc = dalloc_t(h, &h->gcount, (size_t)nb_pad * 64))) return rc;
+    h->geom.nb_groups = (long long)h->rng_blocks * 64;
     if ((rc = dalloc_t(h, &h->tasks, (size_t)nb_pad * kWavesPerBlock))) return rc;
     if ((rc = dalloc_t(h, &h->ntasks, 1))) return rc;
     HIP_OR(hipEventCreateWithFlags(&h->ev_counted, hipEventDisableTiming), DF_EHIP);
@@ -1361,6 +1435,20 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         if ((rc = upload(h, djt, jt.data(), jt.size()))) return rc;
         h->geom.jump_block = djb;
         h->geom.jump_thread = djt;
+        // run generation: group gi of a block starts 4*64*gi outputs in, lane l of a group 4*l further
+        std::vector<PcgJumpDev> jg(64), jl(64);
+        for (int i = 0; i < 64; ++i) {
+            const PcgJump a = pcg_jump(4ull * 64 * (uint64_t)i), b = pcg_jump(4ull * (uint64_t)i);
+            jg[i] = PcgJumpDev{a.mult, a.plus};
+            jl[i] = PcgJumpDev{b.mult, b.plus};
+        }
+        PcgJumpDev *djg = nullptr, *djl = nullptr;
+        if ((rc = dalloc_t(h, &djg, 64))) return rc;
+        if ((rc = dalloc_t(h, &djl, 64))) return rc;
+        if ((rc = upload(h, djg, jg.data(), 64))) return rc;
+        if ((rc = upload(h, djl, jl.data(), 64))) return rc;
+        h->geom.jump_gi = djg;
+        h->geom.jump_lane = djl;
     }
     {
         std::vector<LogTabEntry> lt(kLogTab);
@@ -1461,6 +1549,39 @@ int alloc_dense(df_handle *h)
     uint64_t *cs = nullptr;
     if ((rc = dalloc_t(h, &cs, nch * 64))) return rc;
     h->geom.cstate = cs;
+    // Run generation (gen_dense 2): the list cut into pieces of consecutive chunks, at most kRunPiece each and
+    // of near-equal length within a run (a 9-chunk row segment of a strip is one piece, not 8 + 1)
+    constexpr uint32_t kRunPiece = 12;
+    for (int f = 0; f < 2; ++f) {
+        std::vector<RunPiece> pcs;
+        std::vector<uint32_t> pbits((nch + 31) / 32 + 2, 0u);
+        const std::vector<uint32_t> &L = list[f];
+        for (size_t i = 0; i < L.size();) {
+            size_t j = i + 1;
+            while (j < L.size() && L[j] == L[j - 1] + 1) ++j; // run [i, j)
+            const uint32_t run = (uint32_t)(j - i), np = (run + kRunPiece - 1) / kRunPiece;
+            for (uint32_t k = 0, at = 0; k < np; ++k) {
+                const uint32_t n = (run - at) / (np - k) + ((run - at) % (np - k) ? 1 : 0);
+                const uint32_t c0 = L[i + at];
+                pcs.push_back(RunPiece{c0, (uint32_t)(i + at), n, 0});
+                pbits[c0 >> 5] |= 1u << (c0 & 31);
+                at += n;
+            }
+            i = j;
+        }
+        RunPiece *dp = nullptr;
+        uint32_t *dpb = nullptr;
+        if ((rc = dalloc_t(h, &dp, std::max<size_t>(1, pcs.size())))) return rc;
+        if (!pcs.empty() && (rc = upload(h, dp, pcs.data(), pcs.size()))) return rc;
+        if ((rc = dalloc_t(h, &dpb, pbits.size()))) return rc;
+        if ((rc = upload(h, dpb, pbits.data(), pbits.size()))) return rc;
+        h->geom.pieces[f] = dp;
+        h->geom.npieces[f] = (int)pcs.size();
+        h->geom.piece_bits[f] = dpb;
+    }
+    ChunkLoc *cl = nullptr;
+    if ((rc = dalloc_t(h, &cl, nch + 1))) return rc;
+    h->geom.chunk_loc = cl;
     return DF_OK;
 }
 
@@ -1485,6 +1606,7 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
         HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
+        HIP_OR(hipEventCreateWithFlags(&h->ev_xchg, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
         if (const char *e = std::getenv("DFAMD_HALO_OVERLAP")) h->halo_overlap = std::atoi(e);
     }
@@ -1541,6 +1663,7 @@ int step0(df_handle *h)
     // Constructor step 0 (df.cpp:57-62): noise, sweeps, RST; no correlation, no SRA.
     int rc;
     if ((rc = consume_gen(h))) return rc;
+    if ((rc = fused_gen_begin(h))) return rc;
     if ((rc = ypass_unless_done(h))) return rc;
     if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
@@ -1578,6 +1701,7 @@ void destroy(df_handle *h)
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
     if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
+    if (h->ev_xchg) (void)hipEventDestroy(h->ev_xchg);
     if (h->ev_unpacked) (void)hipEventDestroy(h->ev_unpacked);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
@@ -1828,6 +1952,7 @@ int df_filter(df_handle *h, double dt)
     h->prof_call = h->profiling && (h->prof_seq++ % h->profile_every) == 0;
     const bool prof = prof_on(h);
     if ((rc = consume_gen(h))) return rc;
+    if ((rc = fused_gen_begin(h))) return rc;
     ev_record(h, 0);
     if ((rc = ypass_unless_done(h))) return rc;
     ev_record(h, 1);
@@ -2163,7 +2288,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"zunroll", h->zunroll},
         {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ycoop_map", h->ycoop_map}, {"ydepth", h->ydepth},
         {"ylds", h->ylds}, {"ypre", h->ypre}, {"zocc", h->zocc}, {"handoff_batch", h->hb_conf},
-        {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"k3a_fast", h->k3a_fast}};
+        {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"fused_exchange", h->fused_x}, {"k3a_fast", h->k3a_fast}};
     for (const auto &kv : keys)
         if (k == kv.first) {
             *value = kv.second;
@@ -2206,6 +2331,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     }
     else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
+    else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
     else if (k == "ydepth") h->ydepth = value != 0;
     else if (k == "ylds") h->ylds = value < 0 ? 0 : value > 3 ? 3 : value; // noise chunks in flight (0: off)
@@ -2283,7 +2409,8 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             int rc = alloc_dense(h);
             if (rc) return rc;
         }
-        h->gen_dense = value != 0;
+        if (value < 0 || value > 2) return fail(DF_EINVAL, "gen_dense must be 0, 1 (Kc + K3a) or 2 (run generation)");
+        h->gen_dense = value;
     }
     else if (k == "fast_log") {
         if (value < 0 || value > 2) return fail(DF_EINVAL, "fast_log must be 0 (device log), 1 (log_r2) or 2 (glibc_log)");
@@ -2419,7 +2546,8 @@ int df_comm_info(df_handle *h, df_comm_stats *out)
     out->rng_collective = h->split_count && h->rng_comm ? 1 : 0;
     const long long others = (long long)h->rng_chunk * (h->world - 1);
     out->rng_bytes_received =
-        out->rng_collective ? others * (long long)(sizeof(int) + kWavesPerBlock * sizeof(int)) : 0;
+        out->rng_collective ? others * (h->gen_dense == 2 ? 64LL : (long long)(sizeof(int) + kWavesPerBlock * sizeof(int)))
+                            : 0;
     out->rng_blocks_counted = h->split_count ? h->rng_chunk : h->rng_blocks;
     out->rng_blocks_total = h->rng_blocks;
     return DF_OK;

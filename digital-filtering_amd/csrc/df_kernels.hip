@@ -157,11 +157,22 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
         if (gb >= nb_total) {
             if (tid == 0) counts[gb] = 0;
             if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
+            if (g.gcount && tid < 64) g.gcount[(size_t)gb * 64 + tid] = 0;
             continue;
         }
         const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
         int cnt = __builtin_popcount(bits);
         masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
+        if (g.gcount) { // accepted attempts per group of 64 (one ballot each): the run generation's ranks
+            const int lane = tid & 63;
+            int mine = 0;
+#pragma unroll
+            for (int m = 0; m < kRngPerThread; ++m) {
+                const int n = __popcll(__ballot((bits >> m) & 1u));
+                mine = lane == m ? n : mine;
+            }
+            if (lane < kRngPerThread) g.gcount[(size_t)gb * 64 + w * kRngPerThread + lane] = (uint8_t)mine;
+        }
         for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
         if ((tid & 63) == 0) {
             wsum[w] = cnt;
@@ -880,65 +891,42 @@ __device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q
 #else
 #define DF_K3A_ATTR
 #endif
-template <int kDenseG> // chunks per K3a wave (RngGeom::dense_g: 4, 8 or 16)
-__global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                                        RngStateDev *__restrict__ sout)
+
+// One needed 64-rank chunk c of the dense generation: lane l holds rank 64 c + l, whose attempt starts at
+// state s (any value for ranks past the call's end). di: the chunk's index in the host list (chunk_dest).
+// Near-1 lanes go on the wave's LDS stack (top: its uniform height), batches of 64 are finished here.
+__device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long long A, long long c, int di, uint64_t s,
+                                            int lane, bool defer, Near1Slot *stk, int &top,
+                                            RngStateDev *__restrict__ sout)
 {
-    __shared__ Near1Slot stack_all[kRngThreads / 64][128]; // < 64 carried + 64 pushed per chunk
-    const int lane = threadIdx.x & 63, wv = uniform(threadIdx.x >> 6);
-    Near1Slot *stk = stack_all[wv];
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const int nch = g.nchunks[f];
-    const int i0 = (blockIdx.x * (kRngThreads / 64) + wv) * kDenseG;
-    if (i0 >= nch) return;
-    const int ng = min(kDenseG, nch - i0);
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    const uint32_t *lst = g.chunks[f] + i0;
-    const bool defer = g.fast_log == 2;
-    int top = 0; // uniform stack height
-    long long c = uniform((int)lst[0]);
-    uint64_t s = c * 64 + lane < A ? g.cstate[c * 64 + lane] : 0;
-    for (int k = 0; k < ng; ++k) {
-        // the next chunk's states are in flight while this chunk computes
-        const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
-        const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
-        const ChunkDest cd = g.chunk_dest[f] && !g.debug_flags ? g.chunk_dest[f][i0 + k] : ChunkDest{0, 0, 0, -1, 0};
-        if (cd.arr >= 0) { // uniform
-            // fast chunk (host-built ChunkDest): every lane live and not the call's last attempt, both positions
-            // in one r_ys array - no stream position search, no per-lane destination branches
-            double *const base = (cd.arr == 0 ? g.ry[0] : cd.arr == 2 ? g.ry[1] : g.ry[2]) + cd.off;
-            const int e0 = 2 * lane;
-            double *const p0 = base + e0 + (e0 >= cd.wr ? cd.jump : 0);
-            double *const p1 = base + e0 + 1 + (e0 + 1 >= cd.wr ? cd.jump : 0);
-            uint64_t s3f;
-            const PolarAttempt af = polar_draws(s, s3f);
-            const bool nearf = defer && glibc_log_near1(af.r2);
-            const uint64_t nmf = __ballot(nearf);
-            if (nmf) {
-                if (nearf) {
-                    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nmf >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)nmf, 0u));
-                    stk[top + below] = Near1Slot{af.x, af.y, p0, p1};
-                }
-                top += __popcll(nmf);
+    const ChunkDest cd = g.chunk_dest[f] && !g.debug_flags ? g.chunk_dest[f][di] : ChunkDest{0, 0, 0, -1, 0};
+    if (cd.arr >= 0) { // uniform
+        // fast chunk (host-built ChunkDest): every lane live and not the call's last attempt, both positions
+        // in one r_ys array - no stream position search, no per-lane destination branches
+        double *const base = (cd.arr == 0 ? g.ry[0] : cd.arr == 2 ? g.ry[1] : g.ry[2]) + cd.off;
+        const int e0 = 2 * lane;
+        double *const p0 = base + e0 + (e0 >= cd.wr ? cd.jump : 0);
+        double *const p1 = base + e0 + 1 + (e0 + 1 >= cd.wr ? cd.jump : 0);
+        uint64_t s3f;
+        const PolarAttempt af = polar_draws(s, s3f);
+        const bool nearf = defer && glibc_log_near1(af.r2);
+        const uint64_t nmf = __ballot(nearf);
+        if (nmf) {
+            if (nearf) {
+                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nmf >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)nmf, 0u));
+                stk[top + below] = Near1Slot{af.x, af.y, p0, p1};
             }
-            if (!nearf) {
-                const double lg = defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
-                const double mult = sqrt(-2 * lg / af.r2);
-                const double xm = af.x * mult;
-                const double ym = af.y * mult;
-                store_pair(g, p0, p1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
-            }
-            if (top >= 64) { // as below
-                __asm__ volatile("" ::: "memory");
-                near1_batch(g, stk, top, 64, lane);
-                top -= 64;
-                __asm__ volatile("" ::: "memory");
-            }
-            c = cn;
-            s = sn;
-            continue;
+            top += __popcll(nmf);
         }
+        if (!nearf) {
+            const double lg = defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
+            const double mult = sqrt(-2 * lg / af.r2);
+            const double xm = af.x * mult;
+            const double ym = af.y * mult;
+            store_pair(g, p0, p1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
+        }
+    } else {
         const long long rank = c * 64 + lane;
         const uint64_t q = f + 2ull * (uint64_t)rank;
         const uint64_t q0 = f + 128ull * (uint64_t)c; // uniform
@@ -1006,14 +994,208 @@ __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_ke
                 sout->saved = xm;
             }
         }
-        if (top >= 64) { // the stack is wave-private and a wave's LDS ops complete in order
-            __asm__ volatile("" ::: "memory");
-            near1_batch(g, stk, top, 64, lane);
-            top -= 64;
-            __asm__ volatile("" ::: "memory");
-        }
+    }
+    if (top >= 64) { // the stack is wave-private and a wave's LDS ops complete in order
+        __asm__ volatile("" ::: "memory");
+        near1_batch(g, stk, top, 64, lane);
+        top -= 64;
+        __asm__ volatile("" ::: "memory");
+    }
+}
+
+template <int kDenseG> // chunks per K3a wave (RngGeom::dense_g: 4, 8 or 16)
+__global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                        RngStateDev *__restrict__ sout)
+{
+    __shared__ Near1Slot stack_all[kRngThreads / 64][128]; // < 64 carried + 64 pushed per chunk
+    const int lane = threadIdx.x & 63, wv = uniform(threadIdx.x >> 6);
+    Near1Slot *stk = stack_all[wv];
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const int nch = g.nchunks[f];
+    const int i0 = (blockIdx.x * (kRngThreads / 64) + wv) * kDenseG;
+    if (i0 >= nch) return;
+    const int ng = min(kDenseG, nch - i0);
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    const uint32_t *lst = g.chunks[f] + i0;
+    const bool defer = g.fast_log == 2;
+    int top = 0; // uniform stack height
+    long long c = uniform((int)lst[0]);
+    uint64_t s = c * 64 + lane < A ? g.cstate[c * 64 + lane] : 0;
+    for (int k = 0; k < ng; ++k) {
+        // the next chunk's states are in flight while this chunk computes
+        const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
+        const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
+        dense_chunk(g, f, A, c, i0 + k, s, lane, defer, stk, top, sout);
         c = cn;
         s = sn;
+    }
+    if (top > 0) {
+        __asm__ volatile("" ::: "memory");
+        near1_batch(g, stk, top, top, lane);
+    }
+}
+
+// ---------------------------------------------------------------- run generation (gen_dense 2)
+//
+// The dense form above needs every accepted attempt's state in cstate (Kc): with split counting Kc recomputes
+// the accept flags of every attempt wave that feeds a needed chunk (a whole wave of 1024 attempts for a few
+// chunks: 40 us of a c4/8 table rank, profiles/r3/bl) behind a chain of scan kernels. The run form counts per
+// 64-attempt group instead (K1, one ballot each; the split-counting exchange carries these bytes), scans them
+// (K2g), and locates where each piece of consecutive needed chunks starts (K2l: group G and the accepts of G
+// before the piece's first rank). One wave per piece (K3r) then walks the groups from there: each lane tests
+// its attempt of the group (K1's mask on one GPU, the same float screen under split counting), accepted lanes
+// of the piece append their state to a wave-private 128-slot LDS ring in rank order, and each completed chunk
+// goes through dense_chunk (the same draws, transform and destinations as K3a: bit-identical noise). A piece
+// of n chunks walks ~1.27 n + 1 groups; no cstate round trip, no per-wave pass over the whole stream.
+
+// the sum of the 16 bytes of v (each <= 64)
+__device__ __forceinline__ int byte_sum16(uint4 v)
+{
+    uint32_t t = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t += (w[i] & 0x00FF00FFu) + ((w[i] >> 8) & 0x00FF00FFu); // two 16-bit lanes
+    return (int)((t & 0xFFFFu) + (t >> 16));
+}
+
+// K2g: exclusive scan of the attempt blocks' accept counts (each the sum of its 64 group counts) in runs of
+// 1024 blocks (offsets[b], part[run] = the run's total), as rng_scan_local_kernel; K2l adds the runs before.
+__global__ __launch_bounds__(256) void rng_gscan_kernel(const uint8_t *__restrict__ gcount,
+                                                        long long *__restrict__ offsets, long long *__restrict__ part,
+                                                        int nblocks)
+{
+    __shared__ long long wsum[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int b0 = blockIdx.x * 1024 + tid * 4;
+    int v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v[i] = 0;
+        if (b0 + i < nblocks) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(gcount + (size_t)(b0 + i) * 64);
+            v[i] = byte_sum16(q[0]) + byte_sum16(q[1]) + byte_sum16(q[2]) + byte_sum16(q[3]);
+        }
+    }
+    const long long t = (long long)v[0] + v[1] + v[2] + v[3];
+    long long x = t; // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    long long excl = x - t;
+    for (int ww = 0; ww < w; ++ww) excl += wsum[ww];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (b0 + i < nblocks) offsets[b0 + i] = excl;
+        excl += v[i];
+    }
+    if (tid == 255) part[blockIdx.x] = excl; // run total
+}
+
+// K2l: one wave per attempt block. The block's first rank (its run offset plus the totals of the runs
+// before it: no single-block pass over the run totals), then per lane l the ranks [lo, hi) of group 64 b + l;
+// a piece whose first chunk c starts in there (64 c in [lo, hi)) gets chunk_loc[c] = {G, 64 c - lo}. Also the
+// attempt-shortage check (last block) and the normal cached by the previous call (stream position 0).
+__global__ __launch_bounds__(256) void rng_locate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                         const long long *__restrict__ offsets,
+                                                         const long long *__restrict__ part, int nb_scan,
+                                                         int *__restrict__ err)
+{
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (blockDim.x / 64) + uniform(threadIdx.x >> 6);
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    if (b == 0 && lane == 0 && f) {
+        double *d = stream_dest(g, stream_pos(g, 0));
+        if (d) *d = sin->saved * 1.0 + 0.0;
+    }
+    if (b >= nb_scan) return;
+    long long pre = 0;
+    for (int r = lane; r < (b >> 10); r += 64) pre += part[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    const long long Pb = offsets[b] + pre;
+    const int cnt = g.gcount[(size_t)b * 64 + lane];
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+    }
+    const long long lo = Pb + incl - cnt, hi = Pb + incl;
+    if (b == nb_scan - 1 && lane == 63 && hi < A) *err = 1; // not enough attempts launched: host re-sizes
+    if (cnt > 0 && lo < A) {
+        const long long c = (lo + 63) >> 6; // the first chunk starting at or after lo (c <= the last chunk + 1)
+        if ((c << 6) < hi && ((g.piece_bits[f][c >> 5] >> (c & 31)) & 1u))
+            g.chunk_loc[c] = ChunkLoc{b * 64 + lane, (int)((c << 6) - lo)};
+    }
+}
+
+// K3r: one wave per piece (see above). The ring holds the state one step into each attempt (s1: the screen
+// walks s1 and s3 with one multiply-add each per group); s0 = one step back when the chunk is generated.
+__global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+                                                                      RngStateDev *__restrict__ sout,
+                                                                      const uint16_t *__restrict__ masks)
+{
+    __shared__ Near1Slot stack_all[kRngThreads / 64][128];
+    __shared__ uint64_t ring_all[kRngThreads / 64][128];
+    const int lane = threadIdx.x & 63, wv = uniform(threadIdx.x >> 6);
+    Near1Slot *stk = stack_all[wv];
+    uint64_t *ring = ring_all[wv];
+    const uint64_t f = (uint64_t)sin->saved_flag;
+    const int p = blockIdx.x * (kRngThreads / 64) + wv;
+    if (p >= g.npieces[f]) return;
+    const RunPiece pc = g.pieces[f][p];
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    const bool defer = g.fast_log == 2;
+    const long long c0 = uniform((int)pc.c0), cend = c0 + uniform((int)pc.n);
+    const ChunkLoc loc = g.chunk_loc[c0];
+    long long G = uniform(loc.G);
+    long long R = c0 * 64 - uniform(loc.skip); // rank of group G's first accepted attempt
+    const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
+    // lane's attempt 64 G + lane: its start state s0, then s1 (1 step) and s3 (3 steps) for the screen
+    uint64_t s1, s3;
+    {
+        const uint64_t S = sin->state;
+        const PcgJumpDev jb = g.jump_block[G >> 6], jg = g.jump_gi[G & 63], jl = g.jump_lane[lane];
+        const uint64_t s0 = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
+        s1 = s0 * kPcgMult + kPcgInc;
+        s3 = s1 * kPcgMult2 + kPcgInc2;
+    }
+    long long c = c0;
+    int top = 0;
+    while (c < cend && G < g.nb_groups) { // uniform; the group bound only matters after a shortage (err set)
+        bool acc;
+        if (g.recount) {
+            const int v = polar_screen13(s1, s3);
+            acc = v > 0;
+            if (v < 0) { // ~2e-5 of the attempts: the exact double test (random.tcc:1822-1826), as K1
+                uint64_t s0 = (s1 - kPcgInc) * kPcgMultInv;
+                acc = polar_attempt(s0).accept;
+            }
+        } else {
+            const long long b = G >> 6;
+            const int gi = (int)(G & 63);
+            acc = (masks[(size_t)b * kRngThreads + (gi >> 4) * 64 + lane] >> (gi & 15)) & 1u;
+        }
+        const uint64_t m = __ballot(acc);
+        const long long rank = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = s1;
+        R += __popcll(m);
+        ++G;
+        s1 = g.next_mult * s1 + g.next_plus1;
+        s3 = g.next_mult * s3 + g.next_plus3;
+        __asm__ volatile("" ::: "memory"); // wave-private ring: only the compiler must keep the order
+        while (c < cend && R >= min((c + 1) * 64, A)) { // every rank of chunk c is in the ring
+            const uint64_t s = (ring[(c * 64 + lane) & 127] - kPcgInc) * kPcgMultInv;
+            dense_chunk(g, f, A, c, (int)pc.li0 + (int)(c - c0), s, lane, defer, stk, top, sout);
+            ++c;
+        }
+        __asm__ volatile("" ::: "memory");
     }
     if (top > 0) {
         __asm__ volatile("" ::: "memory");
@@ -1092,6 +1274,19 @@ __global__ __launch_bounds__(1024) void rng_scan_plan_small_kernel(RngGeom g, co
     if (tid == 0) *ntasks = base_sh;
 }
 
+__global__ void replicate_share_kernel(uint8_t *__restrict__ buf, size_t share, int world, int rank)
+{
+    const size_t n = share * (size_t)world;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        if (i / share != (size_t)rank) buf[i] = buf[(size_t)rank * share + i % share];
+}
+
+hipError_t launch_replicate_share(uint8_t *buf, size_t share, int world, int rank, hipStream_t st)
+{
+    hipLaunchKernelGGL(replicate_share_kernel, dim3(256), dim3(256), 0, st, buf, share, world, rank);
+    return hipGetLastError();
+}
+
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
@@ -1111,6 +1306,15 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 #else
     constexpr bool small_ok = true;
 #endif
+    if (g.gen_dense == 2) { // run generation: K2g, K2l, K3r
+        hipLaunchKernelGGL(rng_gscan_kernel, dim3(nparts), dim3(256), 0, st, g.gcount, offsets, part, nb_scan);
+        hipLaunchKernelGGL(rng_locate_kernel, dim3((nb_scan + 3) / 4), dim3(256), 0, st, g, st_in, offsets, part,
+                           nb_scan, err);
+        const int np = g.npieces[0] > g.npieces[1] ? g.npieces[0] : g.npieces[1];
+        hipLaunchKernelGGL(rng_run_generate_kernel, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in, st_out,
+                           masks);
+        return hipGetLastError();
+    }
     if (g.gen_dense) {
         if (small_ok && nb_scan <= 1024 && nb_total <= 1024)
             hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,

@@ -26,6 +26,9 @@ namespace dfamd {
 
 constexpr uint64_t kPcgMult = 6364136223846793005ULL;
 constexpr uint64_t kPcgInc = 1442695040888963407ULL;
+// kPcgMult^-1 mod 2^64: the state one step back, s = (s' - kPcgInc) * kPcgMultInv
+constexpr uint64_t kPcgMultInv = 0xc097ef87329e28a5ULL;
+static_assert(kPcgMult * kPcgMultInv == 1ULL, "pcg multiplier inverse");
 
 DF_HD uint32_t pcg_output(uint64_t s)
 {

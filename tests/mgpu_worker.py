@@ -27,6 +27,8 @@ def main():
         h.set_tuning("rng_replicate", int(spec["replicate"]))
     if "halo_overlap" in spec:  # 0: pack, send/recv, unpack and the whole z-pass as one chain on the stream
         h.set_tuning("halo_overlap", int(spec["halo_overlap"]))
+    for k, v in spec.get("tuning", {}).items():  # e.g. gen_dense 2: run generation + fused exchange
+        h.set_tuning(k, int(v))
     for dt in spec["dts"]:
         h.filter(dt)
     h.sync()

@@ -107,16 +107,31 @@ def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
     check_world(outs, world, replicate, Nz=Nz)
 
 
-@pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 0)])
-def test_rccl_c4_real_partition_emulated(mode, replicate):
+@pytest.mark.parametrize("mode,replicate,tuning", [("packed", 1, {}), ("table", 0, {}), ("table", 0, {"gen_dense": 2})])
+def test_rccl_c4_real_partition_emulated(mode, replicate, tuning):
     """The partition the driver's 8-GPU bench runs first: BASELINE configs[3] (c4,
     2048 x 8192, N 4-64) in eight 2048 x 1024 strips, each rank's 3.1 MB halos per side through the
     product's grouped ncclSend/ncclRecv (RCCL socket transport between emulated hosts on one GPU), every
     strip bit-equal to the whole plane run unsplit after step 0 and two calls."""
     if n_gpus() < 1:
         pytest.skip("needs a GPU")
-    outs = run_world(8, mode, replicate, Ny=2048, Nz=8192, N_min=4, N_max=64, dts=(1e-8, 1e-5), emulate=True)
+    outs = run_world(8, mode, replicate, Ny=2048, Nz=8192, N_min=4, N_max=64, dts=(1e-8, 1e-5), emulate=True,
+                     extra=dict(tuning=tuning))
     check_world(outs, 8, replicate, Nz=8192)
     assert sorted(o["columns"] for o in outs) == [[r * 1024, (r + 1) * 1024] for r in range(8)]
     for o in outs:
         assert o["comm"]["halo_bytes_sent"] == o["comm"]["halo_peers"] * 2048 * 64 * 3 * 8, o["comm"]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_rccl_run_generation_emulated(world, fused):
+    """Table mode with split counting and the run generation (gen_dense 2): the group counts of the next
+    generation travel inside the call's halo group (fused_exchange 1, one grouped RCCL operation per call) or
+    in an all-gather of their own (0); every strip bit-equal to the unsplit plane."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(world, "table", 0, emulate=True, extra=dict(tuning=dict(gen_dense=2, fused_exchange=fused)))
+    check_world(outs, world, 0)
+    for o in outs:
+        assert o["comm"]["rng_bytes_received"] == o["comm"]["rng_blocks_counted"] * (world - 1) * 64

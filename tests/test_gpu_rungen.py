@@ -1,0 +1,77 @@
+"""Run generation (gen_dense 2, round 4): group counts (K1) -> K2g scan -> K2l locate -> K3r one wave per
+piece of consecutive needed chunks, with K1's masks on one GPU and the float screen recomputed under split
+counting. Every field and the stream state bit for bit against the oracle (and so the reference), on planes
+whose pieces start mid-group, wrap rows inside a chunk, end the call, and carry either parity of the cached
+normal; and split over in-process z-strips (each strip generates only its own columns' chunks)."""
+import numpy as np
+import pytest
+
+import dfamd
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("u", "v", "w", "T", "rho")
+
+
+def force_run_form(monkeypatch):
+    # small planes otherwise take the fused-plan / split-wave K3 (no dense generation)
+    for k, v in (("DFAMD_GEN_DENSE", "2"), ("DFAMD_FUSE_PLAN", "0"), ("DFAMD_GEN_SPLIT", "1")):
+        monkeypatch.setenv(k, v)
+
+
+def check(hs, o, what):
+    got_state = [h.rng_state() for h in hs]
+    assert all(s == o.rng.state for s in got_state), (what, got_state, o.rng.state)
+    for k in FIELDS:
+        got = np.concatenate([h.field(k) for h in hs], axis=1)
+        ref = o.field(k)
+        if not np.array_equal(got, ref):
+            bad = np.argwhere(got != ref)
+            raise AssertionError(f"{what} {k}: {len(bad)} cells differ, first {tuple(bad[0])}")
+
+
+@pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90), (37, 129, 2, 10), (40, 133, 2, 8),
+                                  (300, 260, 2, 24), (2, 1, 2, 2)])
+def test_run_generation_single_gpu_matches_oracle(monkeypatch, spec):
+    force_run_form(monkeypatch)
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=31)
+    g = dfamd.DigitalFilter(plane="synthetic", Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=31,
+                            device=0, coeff_mode="table")
+    assert g.get_tuning("gen_dense") == 2
+    check([g], o, "step0")
+    flags = set()
+    for i, dt in enumerate((1e-8, 1e-8, 1e-5, 1e-8, 1e-8)):
+        o.filter(dt)
+        g.filter(dt)
+        flags.add(g.rng_state()[1])
+        check([g], o, f"call {i}")
+    print("saved flags seen:", sorted(flags))
+
+
+@pytest.mark.parametrize("world,Nz", [(2, 700), (3, 1100), (4, 1700), (8, 2048)])
+def test_run_generation_split_counting_strips_match_oracle(monkeypatch, world, Nz):
+    # in-process strips count 1/world of the attempt blocks each and exchange group counts (device copies in
+    # place of the all-gather); every strip recomputes the accept flags of the groups its pieces walk
+    force_run_form(monkeypatch)
+    spec = dict(plane="synthetic", Ny=96, Nz=Nz, N_min=4, N_max=16, seed=8, device=0, coeff_mode="table")
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=96, Nz=Nz, N_min=4, N_max=16, seed=8)
+    hs = dfamd.create_group(world, **spec)
+    check(hs, o, "step0")
+    for i in range(3):
+        o.filter(1e-8)
+        dfamd.filter_group(hs, 1e-8)
+        check(hs, o, f"call {i}")
+
+
+def test_run_generation_switch_forms_mid_run(monkeypatch):
+    # gen_dense 0 / 1 / 2 switched between calls on one handle: the noise of every form is the same bits
+    force_run_form(monkeypatch)
+    spec = (200, 300, 4, 24)
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=5)
+    g = dfamd.DigitalFilter(plane="synthetic", Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=5,
+                            device=0, coeff_mode="table")
+    for i, form in enumerate((1, 2, 0, 2, 2, 1)):
+        g.set_tuning("gen_dense", form)
+        o.filter(1e-8)
+        g.filter(1e-8)
+        check([g], o, f"call {i} form {form}")

@@ -5,7 +5,7 @@
 #   tools/gpu_job.sh TAG STEP [STEP ...]
 #
 # STEP                        runs                                                         limit
-#   tests[=PYTEST_ARGS]       python -u -m pytest tests -m gpu -x -v PYTEST_ARGS           1100 s
+#   tests[=PYTEST_ARGS]       python -u -m pytest PYTEST_ARGS (default: tests) -m gpu -x -v 1100 s
 #   bench[=BENCH_ARGS]        python3 bench.py BENCH_ARGS            -> bench.json         900 s
 #   bench8emu[=BENCH_ARGS]    DFAMD_EMULATE_HOSTS=1 python3 bench.py --gpus 8 BENCH_ARGS  900 s
 #   strip[=ARGS]              python3 tools/strip_timing.py ARGS                           400 s
@@ -30,8 +30,8 @@ for step in "$@"; do
   base="$O/${i}_${name}"
   echo "[gpu_job $(date +%T)] step $i: $name $arg"
   case $name in
-    tests) timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 \
-             --timeout-method thread $arg > "$base.log" 2>&1; rc=$?; tail -3 "$base.log" ;;
+    tests) timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -x -v -p no:cacheprovider --timeout 300 \
+             --timeout-method thread > "$base.log" 2>&1; rc=$?; tail -3 "$base.log" ;;
     bench) timeout -k 10 900 python3 bench.py $arg > "$base.json" 2> "$base.log"; rc=$?
            [ $rc -eq 0 ] && python3 tools/bench_summary.py "$base.json" ;;
     bench8emu) start=$(date +%s)

@@ -11,6 +11,7 @@
 #   strip[=ARGS]              python3 tools/strip_timing.py ARGS                           400 s
 #   prof[=BENCH_ARGS]         rocprofv3 --kernel-trace --stats -- python3 bench.py ...     600 s
 #   py=SCRIPT[,ARGS]          python3 SCRIPT ARGS (commas become spaces)                   400 s
+#   rocpy=SCRIPT[,ARGS]       rocprofv3 --kernel-trace --stats -- python3 SCRIPT ARGS       400 s
 #   smoke                     __graft_entry__.smoke()                                      300 s
 # Outputs: gpurun_out/TAG/<i>_<step>.{log,json}.
 set -o pipefail
@@ -44,6 +45,10 @@ for step in "$@"; do
           [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && head -25 "$base.split.csv" ;;
     py) set -- $arg; script=$1; shift
         timeout -k 10 400 python3 "$script" "$@" > "$base.log" 2>&1; rc=$?; tail -30 "$base.log" ;;
+    rocpy) set -- $arg; script=$1; shift
+        (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$base.d" -o run -- \
+            python3 "$ROOT/$script" "$@" > "$base.log" 2>&1); rc=$?
+        [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && head -25 "$base.split.csv" ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$base.log" 2>&1; rc=$?; tail -2 "$base.log" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac

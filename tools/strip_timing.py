@@ -27,7 +27,7 @@ p.add_argument("--mode", default="packed", choices=["packed", "table"])
 p.add_argument("--replicate", type=int, default=1)
 p.add_argument("--ns", default="1,2,4,8")
 p.add_argument("--calls", type=int, default=20)
-p.add_argument("--tune", default="", help="k=v,... df_set_tuning before the warm-up")
+p.add_argument("--tune", default="", help="k=v:k=v... df_set_tuning before the warm-up")
 a = p.parse_args()
 os.environ["DFAMD_RNG_REPLICATE"] = str(a.replicate)
 import dfamd  # noqa: E402
@@ -37,7 +37,7 @@ for N in [int(x) for x in a.ns.split(",")]:
     for rank in sorted({0, N // 2}):
         f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=4, N_max=64, seed=1, device=0,
                                 rank=rank, world=N, coeff_mode=a.mode)
-        for kv in filter(None, a.tune.split(",")):
+        for kv in filter(None, a.tune.split(":")):
             f.set_tuning(kv.split("=")[0], int(kv.split("=")[1]))
         for _ in range(3):
             f.filter(1e-8)

@@ -59,6 +59,14 @@ int fail(int code, const std::string &msg)
         if (r_ != ncclSuccess) return fail(DF_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(r_));   \
     } while (0)
 
+// Run generation share record (RngGeom::xbuf): 64 group counts per block, int32 block prefixes, int64 total.
+void record_layout(long long chunk, long long *stride, long long *lp_off, long long *tot_off)
+{
+    *lp_off = chunk * 64;
+    *tot_off = (*lp_off + chunk * 4 + 7) / 8 * 8;
+    *stride = (*tot_off + 8 + 15) / 16 * 16;
+}
+
 struct CompDev {
     int Nyp = 0, Nzp = 0, rz_pitch = 0;
     double *ry[kMaxNoiseSets] = {}, *rz[kMaxNoiseSets] = {}; // noise set g % nsets feeds generation g
@@ -155,7 +163,7 @@ struct df_handle {
     long long *part = nullptr; // K2a run totals -> run prefixes (K2b)
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
     int *wave_counts = nullptr; // accepted attempts per wave of each block (K1 -> K2c)
-    uint8_t *gcount = nullptr;  // accepted attempts per 64-attempt group (K1 -> K2g/K2l/K3r, gen_dense 2)
+    uint8_t *xbuf = nullptr;    // run generation: the shares' records (group counts, block prefixes, totals)
     WaveTask *tasks = nullptr;  // waves K3 runs (K2c)
     int *ntasks = nullptr;
     int *err_dev = nullptr;   // mapped host memory: [0] RNG ran short, [1] gather indices skipped, [2] halo loopback mismatches
@@ -483,7 +491,14 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
     g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? h->gen_dense : 0;
-    g.gcount = g.gen_dense == 2 ? h->gcount : nullptr; // K1 writes the group counts the run form scans
+    if (g.gen_dense == 2) { // K1 writes the group counts of its share's record, K2s the share's prefix
+        g.xbuf = h->xbuf;
+        g.xworld = h->split_count ? h->world : 1;
+        g.xchunk = h->split_count ? h->rng_chunk : h->rng_blocks;
+        record_layout(g.xchunk, &g.xstride, &g.xlp_off, &g.xtot_off);
+    } else {
+        g.xbuf = nullptr;
+    }
     if (!h->k3a_fast) g.chunk_dest[0] = g.chunk_dest[1] = nullptr;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
@@ -501,6 +516,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
         HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, h->rank * h->rng_chunk, h->rng_chunk,
                                 h->rng_blocks, rs),
                DF_EHIP);
+    if (g.gen_dense == 2) HIP_OR(launch_rng_share_scan(g, h->counts, h->split_count ? h->rank : 0, rs), DF_EHIP);
     return DF_OK;
 }
 
@@ -575,8 +591,8 @@ int launch_gen_group(std::vector<df_handle *> &hs)
                                   (size_t)h->rng_chunk * kWavesPerBlock * sizeof(int), hipMemcpyDefault, rss[r]),
                    DF_EHIP);
             if (gs[r].gen_dense == 2)
-                HIP_OR(hipMemcpyAsync(h->gcount + at * 64, hs[o]->gcount + at * 64, (size_t)h->rng_chunk * 64,
-                                      hipMemcpyDefault, rss[r]),
+                HIP_OR(hipMemcpyAsync(h->xbuf + (size_t)o * gs[r].xstride, hs[o]->xbuf + (size_t)o * gs[r].xstride,
+                                      (size_t)gs[r].xstride, hipMemcpyDefault, rss[r]),
                        DF_EHIP);
         }
         if ((rc = gen_end(h, gs[r], rss[r]))) return rc;
@@ -599,8 +615,8 @@ int launch_gen(df_handle *h)
         int *mine = h->counts + (size_t)h->rank * h->rng_chunk;
         const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
-        const size_t ngc = (size_t)h->rng_chunk * 64;
-        uint8_t *gmine = h->gcount + (size_t)h->rank * ngc;
+        const size_t ngc = (size_t)g.xstride;
+        uint8_t *gmine = h->xbuf + (size_t)h->rank * ngc;
         if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
             // Never concurrent with the halo send/recv of the other communicator: every rank issues
             // the all-gather only after its own halo group of the call just enqueued has completed,
@@ -608,14 +624,14 @@ int launch_gen(df_handle *h)
             if (h->ev_halo) HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
             NCCL_OR(ncclGroupStart());
             if (g.gen_dense == 2) { // run form: the group counts alone (block counts are their sums)
-                NCCL_OR(ncclAllGather(gmine, h->gcount, ngc, ncclUint8, h->rng_comm, rs));
+                NCCL_OR(ncclAllGather(gmine, h->xbuf, ngc, ncclUint8, h->rng_comm, rs));
             } else {
                 NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
                 NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
             }
             NCCL_OR(ncclGroupEnd());
         } else if (g.gen_dense == 2) { // DFAMD_SOLO_STRIP: this rank's group counts stand in for every share
-            HIP_OR(launch_replicate_share(h->gcount, ngc, h->world, h->rank, rs), DF_EHIP);
+            HIP_OR(launch_replicate_share(h->xbuf, ngc, h->world, h->rank, rs), DF_EHIP);
         } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
             for (int o = 0; o < h->world; ++o)
                 if (o != h->rank) {
@@ -702,8 +718,7 @@ int fused_gen_end(df_handle *h)
         HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
     } else { // solo strip: the same dependency on this call's halo position, the exchange by a stand-in copy
         HIP_OR(hipStreamWaitEvent(rs, h->ev_xchg, 0), DF_EHIP);
-        const size_t ngc = (size_t)h->rng_chunk * 64;
-        HIP_OR(launch_replicate_share(h->gcount, ngc, h->world, h->rank, rs), DF_EHIP);
+        HIP_OR(launch_replicate_share(h->xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
     }
     return gen_end(h, h->pend_g, rs);
 }
@@ -761,9 +776,9 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
 {
     if (h->gen_pending) HIP_OR(hipStreamWaitEvent(st, h->ev_counted, 0), DF_EHIP); // the next generation's counts
     NCCL_OR(ncclGroupStart());
-    if (h->gen_pending) { // fused exchange: the next generation's group counts, in place, in the same group
-        const size_t ngc = (size_t)h->rng_chunk * 64;
-        NCCL_OR(ncclAllGather(h->gcount + (size_t)h->rank * ngc, h->gcount, ngc, ncclUint8, h->comm, st));
+    if (h->gen_pending) { // fused exchange: the next generation's share records, in place, in the same group
+        const size_t ngc = (size_t)h->pend_g.xstride;
+        NCCL_OR(ncclAllGather(h->xbuf + (size_t)h->rank * ngc, h->xbuf, ngc, ncclUint8, h->comm, st));
     }
     if (h->rank > 0) {
         NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
@@ -1409,7 +1424,13 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
     if ((rc = dalloc_t(h, &h->part, (nb_pad + 1023) / 1024))) return rc;
     if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
     if ((rc = dalloc_t(h, &h->wave_counts, (size_t)nb_pad * kWavesPerBlock))) return rc;
-    if ((rc = dalloc_t(h, &h->gcount, (size_t)nb_pad * 64))) return rc;
+    {
+        long long st1 = 0, stw = 0, lo, to;
+        record_layout(h->rng_blocks, &st1, &lo, &to);
+        record_layout(h->rng_chunk, &stw, &lo, &to);
+        if ((rc = dalloc_t(h, &h->xbuf, (size_t)std::max(st1, stw * h->world)))) return rc;
+        if (h->world > 64) return fail(DF_EINVAL, "more than 64 z-strip ranks"); // run generation's share lookup
+    }
     h->geom.nb_groups = (long long)h->rng_blocks * 64;
     if ((rc = dalloc_t(h, &h->tasks, (size_t)nb_pad * kWavesPerBlock))) return rc;
     if ((rc = dalloc_t(h, &h->ntasks, 1))) return rc;
@@ -1554,7 +1575,6 @@ int alloc_dense(df_handle *h)
     constexpr uint32_t kRunPiece = 12;
     for (int f = 0; f < 2; ++f) {
         std::vector<RunPiece> pcs;
-        std::vector<uint32_t> pbits((nch + 31) / 32 + 2, 0u);
         const std::vector<uint32_t> &L = list[f];
         for (size_t i = 0; i < L.size();) {
             size_t j = i + 1;
@@ -1564,24 +1584,16 @@ int alloc_dense(df_handle *h)
                 const uint32_t n = (run - at) / (np - k) + ((run - at) % (np - k) ? 1 : 0);
                 const uint32_t c0 = L[i + at];
                 pcs.push_back(RunPiece{c0, (uint32_t)(i + at), n, 0});
-                pbits[c0 >> 5] |= 1u << (c0 & 31);
                 at += n;
             }
             i = j;
         }
         RunPiece *dp = nullptr;
-        uint32_t *dpb = nullptr;
         if ((rc = dalloc_t(h, &dp, std::max<size_t>(1, pcs.size())))) return rc;
         if (!pcs.empty() && (rc = upload(h, dp, pcs.data(), pcs.size()))) return rc;
-        if ((rc = dalloc_t(h, &dpb, pbits.size()))) return rc;
-        if ((rc = upload(h, dpb, pbits.data(), pbits.size()))) return rc;
         h->geom.pieces[f] = dp;
         h->geom.npieces[f] = (int)pcs.size();
-        h->geom.piece_bits[f] = dpb;
     }
-    ChunkLoc *cl = nullptr;
-    if ((rc = dalloc_t(h, &cl, nch + 1))) return rc;
-    h->geom.chunk_loc = cl;
     return DF_OK;
 }
 
@@ -2545,9 +2557,11 @@ int df_comm_info(df_handle *h, df_comm_stats *out)
     out->halo_bytes_sent = split ? (long long)out->halo_peers * (long long)h->halo_elems * 8 : 0;
     out->rng_collective = h->split_count && h->rng_comm ? 1 : 0;
     const long long others = (long long)h->rng_chunk * (h->world - 1);
-    out->rng_bytes_received =
-        out->rng_collective ? others * (h->gen_dense == 2 ? 64LL : (long long)(sizeof(int) + kWavesPerBlock * sizeof(int)))
-                            : 0;
+    long long rec = 0, lo = 0, to = 0;
+    record_layout(h->rng_chunk, &rec, &lo, &to);
+    out->rng_bytes_received = !out->rng_collective ? 0
+                              : h->gen_dense == 2 ? rec * (h->world - 1)
+                                                  : others * (long long)(sizeof(int) + kWavesPerBlock * sizeof(int));
     out->rng_blocks_counted = h->split_count ? h->rng_chunk : h->rng_blocks;
     out->rng_blocks_total = h->rng_blocks;
     return DF_OK;

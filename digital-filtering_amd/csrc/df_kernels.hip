@@ -157,13 +157,16 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
         if (gb >= nb_total) {
             if (tid == 0) counts[gb] = 0;
             if (tid < kRngThreads / 64) wave_counts[(size_t)gb * (kRngThreads / 64) + tid] = 0;
-            if (g.gcount && tid < 64) g.gcount[(size_t)gb * 64 + tid] = 0;
+            if (g.xbuf && tid < 64) {
+                const int sh = gb / g.xchunk;
+                g.xbuf[(size_t)sh * g.xstride + (size_t)(gb - sh * g.xchunk) * 64 + tid] = 0;
+            }
             continue;
         }
         const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
         int cnt = __builtin_popcount(bits);
         masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
-        if (g.gcount) { // accepted attempts per group of 64 (one ballot each): the run generation's ranks
+        if (g.xbuf) { // accepted attempts per group of 64 (one ballot each) into the share's record (run form)
             const int lane = tid & 63;
             int mine = 0;
 #pragma unroll
@@ -171,7 +174,9 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
                 const int n = __popcll(__ballot((bits >> m) & 1u));
                 mine = lane == m ? n : mine;
             }
-            if (lane < kRngPerThread) g.gcount[(size_t)gb * 64 + w * kRngPerThread + lane] = (uint8_t)mine;
+            const int sh = gb / g.xchunk;
+            if (lane < kRngPerThread)
+                g.xbuf[(size_t)sh * g.xstride + (size_t)(gb - sh * g.xchunk) * 64 + w * kRngPerThread + lane] = (uint8_t)mine;
         }
         for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
         if ((tid & 63) == 0) {
@@ -1048,35 +1053,18 @@ __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_ke
 // goes through dense_chunk (the same draws, transform and destinations as K3a: bit-identical noise). A piece
 // of n chunks walks ~1.27 n + 1 groups; no cstate round trip, no per-wave pass over the whole stream.
 
-// the sum of the 16 bytes of v (each <= 64)
-__device__ __forceinline__ int byte_sum16(uint4 v)
+// K2s: one share's block prefix. One 1024-thread block over the share's xchunk block counts (K1's per-block
+// totals): the exclusive prefix of each block within the share (int32) and the share's total (int64), written
+// to the share's record. Runs right after K1, before any exchange: with split counting it is each rank's own
+// share, so the records the ranks exchange already carry their prefixes and nothing scans after the exchange.
+__global__ __launch_bounds__(1024) void rng_share_scan_kernel(RngGeom g, const int *__restrict__ counts, int share)
 {
-    uint32_t t = 0;
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) t += (w[i] & 0x00FF00FFu) + ((w[i] >> 8) & 0x00FF00FFu); // two 16-bit lanes
-    return (int)((t & 0xFFFFu) + (t >> 16));
-}
-
-// K2g: exclusive scan of the attempt blocks' accept counts (each the sum of its 64 group counts) in runs of
-// 1024 blocks (offsets[b], part[run] = the run's total), as rng_scan_local_kernel; K2l adds the runs before.
-__global__ __launch_bounds__(256) void rng_gscan_kernel(const uint8_t *__restrict__ gcount,
-                                                        long long *__restrict__ offsets, long long *__restrict__ part,
-                                                        int nblocks)
-{
-    __shared__ long long wsum[4];
+    __shared__ long long wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int b0 = blockIdx.x * 1024 + tid * 4;
-    int v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        v[i] = 0;
-        if (b0 + i < nblocks) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(gcount + (size_t)(b0 + i) * 64);
-            v[i] = byte_sum16(q[0]) + byte_sum16(q[1]) + byte_sum16(q[2]) + byte_sum16(q[3]);
-        }
-    }
-    const long long t = (long long)v[0] + v[1] + v[2] + v[3];
+    const int n = g.xchunk, per = (n + 1023) / 1024;
+    const int b0 = share * n, i0 = min(tid * per, n), i1 = min(i0 + per, n);
+    long long t = 0;
+    for (int i = i0; i < i1; ++i) t += counts[b0 + i];
     long long x = t; // inclusive wave scan
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1087,58 +1075,82 @@ __global__ __launch_bounds__(256) void rng_gscan_kernel(const uint8_t *__restric
     __syncthreads();
     long long excl = x - t;
     for (int ww = 0; ww < w; ++ww) excl += wsum[ww];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (b0 + i < nblocks) offsets[b0 + i] = excl;
-        excl += v[i];
+    uint8_t *rec = g.xbuf + (size_t)share * g.xstride;
+    int *lp = reinterpret_cast<int *>(rec + g.xlp_off);
+    for (int i = i0; i < i1; ++i) {
+        lp[i] = (int)excl;
+        excl += counts[b0 + i];
     }
-    if (tid == 255) part[blockIdx.x] = excl; // run total
+    if (tid == 1023) *reinterpret_cast<long long *>(rec + g.xtot_off) = excl;
 }
 
-// K2l: one wave per attempt block. The block's first rank (its run offset plus the totals of the runs
-// before it: no single-block pass over the run totals), then per lane l the ranks [lo, hi) of group 64 b + l;
-// a piece whose first chunk c starts in there (64 c in [lo, hi)) gets chunk_loc[c] = {G, 64 c - lo}. Also the
-// attempt-shortage check (last block) and the normal cached by the previous call (stream position 0).
-__global__ __launch_bounds__(256) void rng_locate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                         const long long *__restrict__ offsets,
-                                                         const long long *__restrict__ part, int nb_scan,
-                                                         int *__restrict__ err)
+// Where rank T of the call lies, from the share records: the group G (attempts [64 G, 64 G + 64)) whose
+// accepted attempts hold ranks [T - skip, ...). Returns false if T is past every counted attempt. Uniform.
+// Shares' totals -> the share; block prefixes in a 64-block window around the expected block (pi/4 of 4096
+// attempts accepted per block: the window almost always brackets T at once) -> the block; its 64 group
+// counts -> the group.
+__device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &G, int &skip, long long &grand)
 {
-    const int lane = threadIdx.x & 63;
-    const int b = blockIdx.x * (blockDim.x / 64) + uniform(threadIdx.x >> 6);
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    if (b == 0 && lane == 0 && f) {
-        double *d = stream_dest(g, stream_pos(g, 0));
-        if (d) *d = sin->saved * 1.0 + 0.0;
-    }
-    if (b >= nb_scan) return;
-    long long pre = 0;
-    for (int r = lane; r < (b >> 10); r += 64) pre += part[r];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
-    const long long Pb = offsets[b] + pre;
-    const int cnt = g.gcount[(size_t)b * 64 + lane];
-    int incl = cnt;
+    const int W = g.xworld;
+    long long tot = 0;
+    for (int s = lane; s < W; s += 64) tot += *reinterpret_cast<const long long *>(g.xbuf + (size_t)s * g.xstride + g.xtot_off);
+    long long incl = tot; // shares in lane order (W <= 64: checked at create)
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
+        const long long y = __shfl_up(incl, o);
         if (lane >= o) incl += y;
     }
-    const long long lo = Pb + incl - cnt, hi = Pb + incl;
-    if (b == nb_scan - 1 && lane == 63 && hi < A) *err = 1; // not enough attempts launched: host re-sizes
-    if (cnt > 0 && lo < A) {
-        const long long c = (lo + 63) >> 6; // the first chunk starting at or after lo (c <= the last chunk + 1)
-        if ((c << 6) < hi && ((g.piece_bits[f][c >> 5] >> (c & 31)) & 1u))
-            g.chunk_loc[c] = ChunkLoc{b * 64 + lane, (int)((c << 6) - lo)};
+    grand = __shfl(incl, 63);
+    if (T >= grand) return false;
+    const uint64_t ms = __ballot(lane < W && T < incl && T >= incl - tot);
+    const int s = __builtin_ctzll(ms);
+    const long long Tl = T - __shfl(incl - tot, s);
+    const uint8_t *rec = g.xbuf + (size_t)s * g.xstride;
+    const int *lp = reinterpret_cast<const int *>(rec + g.xlp_off);
+    const int n = g.xchunk;
+    int lo = (int)((double)Tl * (1.0 / 3216.990877275948)) - 32; // 4096 * pi / 4 accepts per block
+    lo = max(0, min(lo, n - 64));
+    int b = -1;
+    for (int it = 0; it < 1 << 16; ++it) { // bounded: each step moves the window towards T
+        const int i = lo + lane;
+        const bool le = i < n && (long long)lp[i] <= Tl; // lp is nondecreasing
+        const uint64_t m = __ballot(le);
+        if (m == 0) {
+            if (lo == 0) break; // cannot happen (lp[0] = 0 <= Tl)
+            lo = max(0, lo - 63);
+            continue;
+        }
+        const int last = 63 - __builtin_clzll(m);
+        if (last == 63 && lo + 64 < n) {
+            lo += 63;
+            continue;
+        }
+        b = lo + last;
+        break;
     }
+    if (b < 0) return false;
+    const long long Tb = Tl - __shfl(lp[min(lo + lane, n - 1)], b - lo);
+    const int cnt = rec[(size_t)b * 64 + lane];
+    int gin = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(gin, o);
+        if (lane >= o) gin += y;
+    }
+    const uint64_t mg = __ballot((long long)gin > Tb);
+    if (!mg) return false;
+    const int gl = __builtin_ctzll(mg);
+    skip = (int)(Tb - __shfl(gin - cnt, gl));
+    G = ((long long)s * n + b) * 64 + gl;
+    return true;
 }
 
 // K3r: one wave per piece (see above). The ring holds the state one step into each attempt (s1: the screen
 // walks s1 and s3 with one multiply-add each per group); s0 = one step back when the chunk is generated.
 __global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                       RngStateDev *__restrict__ sout,
-                                                                      const uint16_t *__restrict__ masks)
+                                                                      const uint16_t *__restrict__ masks,
+                                                                      int *__restrict__ err)
 {
     __shared__ Near1Slot stack_all[kRngThreads / 64][128];
     __shared__ uint64_t ring_all[kRngThreads / 64][128];
@@ -1147,14 +1159,22 @@ __global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g
     uint64_t *ring = ring_all[wv];
     const uint64_t f = (uint64_t)sin->saved_flag;
     const int p = blockIdx.x * (kRngThreads / 64) + wv;
+    const long long A = (long long)((g.Q - f + 1) / 2);
+    if (p == 0 && lane == 0 && f) { // the normal cached by the previous call is stream position 0
+        double *d = stream_dest(g, stream_pos(g, 0));
+        if (d) *d = sin->saved * 1.0 + 0.0;
+    }
     if (p >= g.npieces[f]) return;
     const RunPiece pc = g.pieces[f][p];
-    const long long A = (long long)((g.Q - f + 1) / 2);
     const bool defer = g.fast_log == 2;
     const long long c0 = uniform((int)pc.c0), cend = c0 + uniform((int)pc.n);
-    const ChunkLoc loc = g.chunk_loc[c0];
-    long long G = uniform(loc.G);
-    long long R = c0 * 64 - uniform(loc.skip); // rank of group G's first accepted attempt
+    long long G, grand;
+    int skip;
+    const bool found = locate_rank(g, c0 * 64, lane, G, skip, grand);
+    if (p == g.npieces[f] - 1 && lane == 0 && grand < A) *err = 1; // not enough attempts launched: host re-sizes
+    if (!found) return;
+    G = uniform((int)G);
+    long long R = c0 * 64 - uniform(skip); // rank of group G's first accepted attempt
     const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
     // lane's attempt 64 G + lane: its start state s0, then s1 (1 step) and s3 (3 steps) for the screen
     uint64_t s1, s3;
@@ -1274,16 +1294,24 @@ __global__ __launch_bounds__(1024) void rng_scan_plan_small_kernel(RngGeom g, co
     if (tid == 0) *ntasks = base_sh;
 }
 
-__global__ void replicate_share_kernel(uint8_t *__restrict__ buf, size_t share, int world, int rank)
+__global__ void replicate_share_kernel(uint4 *__restrict__ buf, size_t n16, int rank)
 {
-    const size_t n = share * (size_t)world;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-        if (i / share != (size_t)rank) buf[i] = buf[(size_t)rank * share + i % share];
+    const int r = blockIdx.y; // destination record
+    if (r == rank) return;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+        buf[(size_t)r * n16 + i] = buf[(size_t)rank * n16 + i];
 }
 
-hipError_t launch_replicate_share(uint8_t *buf, size_t share, int world, int rank, hipStream_t st)
+hipError_t launch_replicate_share(uint8_t *buf, size_t bytes, int world, int rank, hipStream_t st)
 {
-    hipLaunchKernelGGL(replicate_share_kernel, dim3(256), dim3(256), 0, st, buf, share, world, rank);
+    hipLaunchKernelGGL(replicate_share_kernel, dim3(64, world), dim3(256), 0, st, reinterpret_cast<uint4 *>(buf),
+                       bytes / 16, rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share, hipStream_t st)
+{
+    hipLaunchKernelGGL(rng_share_scan_kernel, dim3(1), dim3(1024), 0, st, g, counts, share);
     return hipGetLastError();
 }
 
@@ -1306,13 +1334,10 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 #else
     constexpr bool small_ok = true;
 #endif
-    if (g.gen_dense == 2) { // run generation: K2g, K2l, K3r
-        hipLaunchKernelGGL(rng_gscan_kernel, dim3(nparts), dim3(256), 0, st, g.gcount, offsets, part, nb_scan);
-        hipLaunchKernelGGL(rng_locate_kernel, dim3((nb_scan + 3) / 4), dim3(256), 0, st, g, st_in, offsets, part,
-                           nb_scan, err);
+    if (g.gen_dense == 2) { // run generation: K3r alone (K2s ran with K1, before any exchange)
         const int np = g.npieces[0] > g.npieces[1] ? g.npieces[0] : g.npieces[1];
         hipLaunchKernelGGL(rng_run_generate_kernel, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in, st_out,
-                           masks);
+                           masks, err);
         return hipGetLastError();
     }
     if (g.gen_dense) {

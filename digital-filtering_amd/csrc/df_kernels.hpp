@@ -65,12 +65,6 @@ struct RunPiece {
     uint32_t c0, li0, n, pad;
 };
 
-// Where a piece's first rank 64 c0 lies: in attempt group G (attempts [64 G, 64 G + 64) of the call) after
-// `skip` of the group's accepted attempts (K2l rng_locate_kernel -> K3r).
-struct ChunkLoc {
-    int G, skip;
-};
-
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
@@ -108,14 +102,17 @@ struct RngGeom {
     // K3a fast chunks (one GPU): per listed chunk, where its 128 positions land when they all go to one r_ys
     // array with at most one row wrap; arr < 0 marks a chunk for the general per-lane path.
     const struct ChunkDest *chunk_dest[2];
-    // Run generation (gen_dense 2): accepted attempts per 64-attempt group (K1; the split-counting exchange),
-    // the pieces of each parity's chunk list, a bitmap of the pieces' first chunks, their group locations,
-    // and jumps to a group inside a block (4 * 64 * gi outputs) and to a lane inside a group (4 * l).
-    uint8_t *gcount;
+    // Run generation (gen_dense 2). The attempt blocks are cut into xworld shares of xchunk blocks (the z-strip
+    // ranks' counting shares; one share on a single GPU); share s has a record of xstride bytes at xbuf +
+    // s * xstride: the accepted attempts of each 64-attempt group of its blocks (uint8, 64 per block; K1), the
+    // share-local exclusive prefix of its block counts (int32 at xlp_off; K2s) and its total (int64 at
+    // xtot_off; K2s). Under split counting the records are what the ranks exchange. Also the pieces of each
+    // parity's chunk list, and jumps to a group inside a block (4 * 64 * gi outputs) and to a lane in a group.
+    uint8_t *xbuf;
+    long long xstride, xlp_off, xtot_off;
+    int xchunk, xworld;
     const RunPiece *pieces[2];
     int npieces[2];
-    const uint32_t *piece_bits[2];
-    ChunkLoc *chunk_loc;
     const PcgJumpDev *jump_gi, *jump_lane;
     long long nb_groups; // groups of the call's attempt blocks (64 per block)
 };
@@ -182,12 +179,14 @@ hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st
 // K1 for blocks [b0, b0+nb) of nb_total (a z-strip rank counts its share only).
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st);
+// K2s (run generation): share `share`'s block prefix and total into its exchange record (after K1).
+hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share, hipStream_t st);
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
                              const int *wave_counts, long long *offsets, long long *part, uint16_t *masks,
                              WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st);
-// DFAMD_SOLO_STRIP stand-in for the split-counting all-gather: rank's share of `share` bytes copied over every
-// other rank's share of buf (one launch, as one collective would be).
-hipError_t launch_replicate_share(uint8_t *buf, size_t share, int world, int rank, hipStream_t st);
+// DFAMD_SOLO_STRIP stand-in for the split-counting all-gather: rank's record of `bytes` (a multiple of 16)
+// copied over every other rank's record of buf (one launch, as one collective would be).
+hipError_t launch_replicate_share(uint8_t *buf, size_t bytes, int world, int rank, hipStream_t st);
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st);
 hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st);
 // Stage API elementwise kernels: op 0 correlate_fields(comp) (df.cpp:408-417),

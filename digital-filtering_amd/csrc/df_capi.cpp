@@ -2345,7 +2345,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on
     else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
-    else if (k == "ydepth") h->ydepth = value != 0;
+    else if (k == "ydepth") h->ydepth = value < 0 ? 0 : value > 2 ? 2 : value;
     else if (k == "ylds") h->ylds = value < 0 ? 0 : value > 3 ? 3 : value; // noise chunks in flight (0: off)
     else if (k == "ylds_nw") h->ylds_nw = value == 8 ? 8 : 4;
     else if (k == "ylds_ch") h->ylds_ch = value == 32 ? 32 : 16;

@@ -1841,6 +1841,176 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
     }
 }
 
+// K4, table mode (row-uniform N per cell: every plane but per-cell grids): the per-wave tile of ypass_kernel with
+// the coefficients from the full symmetric vectors (tabf) and only the paths table mode takes, so the kernel's
+// register budget is set by its hot loop alone (the shared ypass_kernel carried every packed and table path:
+// 105 VGPRs, 4 waves per SIMD, for a loop that needs ~60; round 4). Hot loop on tiles whose R rows share one N:
+// taps in groups of 4 noise rows, the noise KYD groups ahead in a register ring, the group's R + 3
+// coefficients one scalar window (b[t - R + 1 .. t + 3]) loaded one group ahead. Tiles where N steps between
+// their rows take the per-row form with the next two noise rows in flight. Same products, same order as
+// df.cpp:373-375: bit-identical.
+template <int R, int KYD>
+__global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowblk)
+{
+    const int c = blockIdx.y;
+    if (!((a.comps_mask >> c) & 1)) return;
+    const int lane = threadIdx.x & 63;
+    const int per_xcd = gridDim.x >> 3; // XCD-aware order, as ypass_kernel
+    const int b = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    const int tile = uniform(b * 4 + (threadIdx.x >> 6));
+    if (tile >= a.nstrips * nrowblk) return;
+    const int s = tile / nrowblk;
+    const int rb = nrowblk - 1 - (tile - s * nrowblk); // wide stencils (large j) start first
+    const int j0 = rb * R;
+    const int Ny = a.Ny;
+    const int nr = min(R, Ny - j0);
+    const int col = s * kStrip + 2 * lane;
+    const int Pz = a.Pz;
+    if (col >= a.Nz_loc) return; // lanes wholly in the last strip's padding
+    int N[R];
+    const double *tb[R];
+    int Nlo = 1 << 30, Nhi = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        N[r] = 0;
+        tb[r] = a.tabf; // unused for r >= nr
+        if (r < nr) {
+            N[r] = a.Ny_st[c][(size_t)s * Ny + j0 + r];
+            Nlo = min(Nlo, N[r]);
+            Nhi = max(Nhi, N[r]);
+            tb[r] = a.tabf + a.tabf_off[N[r]] + N[r]; // centre of the full vector: tap i at tb[i]
+        }
+    }
+    const double *np = a.ry[c] + (size_t)(j0 + a.Nyp[c]) * Pz + col;
+    double acc0[R], acc1[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0.0;
+    auto noise = [&](int t) { return DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t); };
+    auto predicated = [&](int t) {
+        const double2 n = noise(t);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = t - r;
+            if (r < nr && i >= -N[r] && i <= N[r]) {
+                const double bb = DF_TCOEF(tb[r][i]);
+                acc0[r] += bb * n.x;
+                acc1[r] += bb * n.y;
+            }
+        }
+    };
+    auto body_n = [&](int t, const double2 n) {
+        double bb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) bb[r] = DF_TCOEF(tb[r][t - r]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc0[r] += bb[r] * n.x;
+            acc1[r] += bb[r] * n.y;
+        }
+    };
+    const int tlo = -Nhi, thi = (nr - 1) + Nhi;
+    const bool body_ok = (nr == R) && (R - 1 - Nlo <= Nlo);
+    const int bl = body_ok ? R - 1 - Nlo : thi + 1;
+    const int bh = body_ok ? Nlo : thi;
+    int t = tlo;
+    for (; t < bl; ++t) predicated(t);
+    if (Nlo == Nhi && t + 4 * KYD - 1 <= bh) {
+        constexpr int WN = (R + 3 + 7) / 8 * 8;
+        const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
+        double2 nq[KYD][4];
+        const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
+        const double *nl = np + (ptrdiff_t)t * Pz; // next group to load
+        auto ldn = [&](double2 (&nn)[4]) {
+            nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nl), 0);
+            nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P1), 1);
+            nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P2), 2);
+            nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P3), 3);
+            nl += P4;
+        };
+        auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const double bb = ww[u - r + R - 1];
+                    acc0[r] += bb * nn[u].x;
+                    acc1[r] += bb * nn[u].y;
+                }
+                __builtin_amdgcn_sched_barrier(0); // one tap's products at a time (register pressure)
+            }
+        };
+        const double *wq = cb + t;
+        double w[WN];
+#pragma unroll
+        for (int k = 0; k < WN; ++k) w[k] = DF_TCOEF(wq[k]);
+#pragma unroll
+        for (int g = 0; g < KYD; ++g) ldn(nq[g]);
+        for (; t + 8 * KYD - 1 <= bh; t += 4 * KYD) { // the groups issued below stay within bh
+#pragma unroll
+            for (int g = 0; g < KYD; ++g) {
+                double wn[WN];
+#pragma unroll
+                for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]); // the table is padded past its last vector
+                __builtin_amdgcn_sched_barrier(0);
+                taps(nq[g], w);
+                ldn(nq[g]); // group t + 4 (g + KYD)
+                __builtin_amdgcn_sched_barrier(0);
+                wq += 4;
+#pragma unroll
+                for (int k = 0; k < WN; ++k) w[k] = wn[k];
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < KYD; ++g) { // drain: groups t .. t + 4 KYD - 1, loaded, within bh
+            double wn[WN];
+#pragma unroll
+            for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]);
+            taps(nq[g], w);
+            wq += 4;
+#pragma unroll
+            for (int k = 0; k < WN; ++k) w[k] = wn[k];
+        }
+        t += 4 * KYD;
+    }
+    if (t + 1 <= bh) { // per-row coefficients, the next two noise rows in flight
+        double2 n0 = noise(t), n1 = noise(t + 1);
+        for (; t + 5 <= bh; t += 4) {
+            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            n0 = noise(t + 4);
+            n1 = noise(t + 5);
+            body_n(t + 2, m0);
+            body_n(t + 3, m1);
+        }
+        if (t + 3 <= bh) {
+            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            body_n(t + 2, m0);
+            body_n(t + 3, m1);
+            t += 4;
+        } else {
+            body_n(t, n0);
+            body_n(t + 1, n1);
+            t += 2;
+        }
+    }
+    for (; t <= bh; ++t) body_n(t, noise(t));
+    for (; t <= thi; ++t) predicated(t);
+    write_window(a.ywin_T, a.ywin_W);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (r < nr) {
+            double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + col;
+            if (col + 1 < a.Nz_loc) {
+                if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
+                else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
+            } else if (col < a.Nz_loc) o[0] = acc0[r];
+        }
+    }
+}
+
 // K4, block-cooperative form for long tap chains (packed mode; SweepArgs::ycoop). One BLOCK per
 // (strip, row) tile instead of one wave: the tile's 2N+1 taps go in chunks of 4*KPW; wave w loads taps
 // w, w+4, ... of the chunk (KPW coefficient and noise pairs in flight per wave, 4*KPW per tile), writes
@@ -2231,7 +2401,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     const dim3 grid(blocks, 3);
     if (TABLE && a.per_cell)
         hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
-    else if (!TABLE && a.nt_loads) {
+    else if (TABLE && a.ydepth >= 1) { // ydepth 0: the shared ypass_kernel (A/B only)
+        constexpr int KYD = R <= 2 ? 4 : R == 4 ? 2 : 1;
+        if (a.ydepth >= 2 && R == 4) // timing: 3 groups ahead at 4 rows
+            hipLaunchKernelGGL((ypass_table_kernel<R, 3>), grid, dim3(256), 0, st, a, nrowblk);
+        else
+            hipLaunchKernelGGL((ypass_table_kernel<R, KYD>), grid, dim3(256), 0, st, a, nrowblk);
+    } else if (!TABLE && a.nt_loads) {
         if constexpr (R <= 2) { // deeper rings (16 or 32 taps in flight) for one or two rows per wave
             if (a.yunroll >= 32) {
                 hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 32, false>), grid, dim3(256), 0, st, a, nrowblk);

@@ -83,10 +83,8 @@ struct CompDev {
 };
 
 struct PhaseEvents {
-    hipEvent_t e[8]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end, and the
-                     // prefetched y-pass's start and end (ypre)
+    hipEvent_t e[6]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end
     bool rng = false;
-    bool ypre = false;
     int gens = 0; // generations enqueued during the call: e[4] before the first, e[5] after the last
 };
 
@@ -106,8 +104,6 @@ struct df_handle {
     ncclComm_t comm = nullptr;
     int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
     int rows_per_wave = 8;
-    int nt_loads = 1; // coefficient stream is read once per call: non-temporal (measured +6%)
-    int heavy_first = 1;
     int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
     int ynt_stores = 1; // the y-pass output likewise
@@ -129,9 +125,7 @@ struct df_handle {
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
-    int zocc = 0;        // z-pass register budget (SweepArgs::zocc)
     int ydepth = 1;      // table y-pass, 1-2 rows per wave: 16 noise rows in flight (SweepArgs::ydepth)
-    int ycoop_map = 0;   // row-pair y-pass tiles to XCDs: 0 equal-byte contiguous runs, 1 interleaved (t % 8)
     int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
                          // consecutive tiles, heaviest group first (balance_ycoop2)
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
@@ -143,15 +137,6 @@ struct df_handle {
     int rng_replicate = 1;
     int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
-    // Steady-state filter() as a HIP graph (single-GPU handles): one graph per noise-set parity
-    // holds {y-pass -> z-pass} beside {K1 -> K2a -> K2b -> K2c -> K3 of the next call}, so a call
-    // is one hipGraphLaunch instead of ~10 API calls. Opt-in: measured SLOWER than the two-stream
-    // launches on ROCm 7 / MI355X (c1 43.8 -> 67.9 us per call, c2 table 48 -> 81 us;
-    // profiles/r1/probe/small_plane_latency.jsonl, same box), bit-identical either way.
-    int use_graph = 0;
-    hipGraphExec_t graph[2] = {nullptr, nullptr};
-    double graph_dt[2] = {0, 0};
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
     CompDev c[3];
     double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr, *tabf = nullptr;
@@ -206,17 +191,10 @@ struct df_handle {
     // kHbRestoreCalls calls without such a load the handle returns to hb_conf
     int hb_conf = 1;
     int calls_since_load = 0;
-    int hb_burst = 0; // 1: an epoch's generations enqueued in one burst (measured against spread, profiles/r3/m)
     int nsets = 2;
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
-    // y-pass prefetch (ypre): the next call's y-pass depends only on its noise (not on dt), so it is enqueued
-    // on rng_stream right after that noise and runs beside this call's z-pass; df_filter then runs the
-    // z-pass only. ydone[set]: the generation in that set already holds its y-filtered r_zs interior.
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds)
-    int ylds_nw = 4, ylds_ch = 16;
-    int ypre = 0;
-    bool ydone[kMaxNoiseSets] = {};
     int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
     RngGeom geom{};
     // halo
@@ -353,8 +331,6 @@ SweepArgs sweep_args(df_handle *h)
     a.rho = h->rho;
     a.rowc = h->rowc;
     a.comps_mask = 7;
-    a.nt_loads = h->nt_loads;
-    a.heavy_first = h->heavy_first;
     a.yunroll = h->yunroll;
     a.ywindow = h->ywindow;
     a.ydeep = h->ydeep;
@@ -369,12 +345,8 @@ SweepArgs sweep_args(df_handle *h)
         a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
         a.ycoop2_perm[c] = h->ycoop_order ? h->c[c].ycoop2_perm : nullptr;
     }
-    a.ycoop2_map = h->ycoop_map;
-    a.zocc = h->zocc;
     a.ydepth = h->ydepth;
     a.ylds = h->ylds;
-    a.ylds_nw = h->ylds_nw;
-    a.ylds_ch = h->ylds_ch;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -444,14 +416,12 @@ int drain_profile(df_handle *h)
             h->prof_rng_span += r;
             h->prof_rng_gens += h->ev[i].gens;
         }
-        if (h->ev[i].ypre) (void)hipEventElapsedTime(&t[0], h->ev[i].e[6], h->ev[i].e[7]); // on rng_stream
         h->prof.ypass_ms += t[0];
         h->prof.halo_ms += t[1];
         h->prof.zpass_ms += t[2];
         h->prof.total_ms += tot;
         h->prof.calls++;
         h->ev[i].rng = false;
-        h->ev[i].ypre = false;
         h->ev[i].gens = 0;
     }
     h->ev_used = 0;
@@ -465,7 +435,7 @@ int drain_profile(df_handle *h)
 // ---------------------------------------------------------------- phases
 
 // Epochs of the noise pipeline: with hb == 1 every generation is its own epoch (absolute index, so the
-// event parity is the noise-set parity, as the graph path assumes); with hb > 1, epochs of hb
+// event parity is the noise-set parity); with hb > 1, epochs of hb
 // generations counted from gen_base.
 constexpr int kHbRestoreCalls = 16;
 
@@ -520,16 +490,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     return DF_OK;
 }
 
-// ypre applies to single-plane handles (no strips: the halo exchange sits between the two passes)
-bool ypre_active(const df_handle *h) { return h->ypre && h->world == 1 && !h->group; }
-
-// A visible step's y-pass, unless the generation it consumes already ran it (ypre).
 int phase_ypass(df_handle *h, int comps_mask);
-int ypass_unless_done(df_handle *h)
-{
-    if (h->ydone[h->cur]) return DF_OK;
-    return phase_ypass(h, 7);
-}
 
 int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
@@ -542,22 +503,6 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
                              h->rng_blocks, nb_scan, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5);
-    const int set = gen_set(h, gi);
-    h->ydone[set] = false;
-    if (ypre_active(h)) { // this generation's y-pass, under the current call's z-pass
-        const int saved = h->cur;
-        h->cur = set;
-        SweepArgs a = sweep_args(h);
-        h->cur = saved;
-        a.comps_mask = 7;
-        if (prof_on(h)) ev_record(h, 6);
-        HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, rs), DF_EHIP);
-        if (prof_on(h)) {
-            ev_record(h, 7);
-            h->ev[h->ev_used].ypre = true;
-        }
-        h->ydone[set] = true;
-    }
     if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
     h->gen_launched++;
@@ -666,8 +611,8 @@ int consume_gen(df_handle *h)
 }
 
 // After a visible step's sweeps are enqueued: generations up to hb steps ahead, under those sweeps.
-// hb_burst 1 enqueues a whole epoch at its predecessor's first step instead (one burst of hb
-// generations); spread (the default) enqueues one per step, so the last generation of epoch e + 1 goes
+// One generation is enqueued per step (an epoch enqueued as one burst measured no better, profiles/r3/m),
+// so the last generation of epoch e + 1 goes
 // under the last step of epoch e, just before epoch e + 1 waits for it.
 int fused_gen_end(df_handle *h);
 int prefetch_gen(df_handle *h)
@@ -675,11 +620,8 @@ int prefetch_gen(df_handle *h)
     if (int rc = fused_gen_end(h)) return rc;
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
-    long long need = h->gen_used + h->hb;
-    if (h->hb_burst && h->hb > 1) {
-        if (gen_pos(h, gi) != 0) return DF_OK;
-        need = h->gen_base + (gen_epoch(h, gi) + 2) * h->hb;
-    }
+    (void)gi;
+    const long long need = h->gen_used + h->hb;
     int rc;
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
@@ -951,12 +893,9 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
     h->rows_per_wave = cfg->rows_per_wave; // 0: chosen from the plane's shape after setup (below)
     // tuning knobs for in-process A/B experiments (tools/ab.py); defaults are the measured best
-    if (const char *e = std::getenv("DFAMD_NT_LOADS")) h->nt_loads = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_HEAVY_FIRST")) h->heavy_first = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YUNROLL")) h->yunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_ZUNROLL")) h->zunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_GRAPH")) h->use_graph = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
     // Table mode splits the counting (one small all-gather of counts beside the halo): its sweeps are
     // VALU-bound like the RNG, so every rank counting the whole stream shows (one rank of a c4 split
@@ -1099,8 +1038,6 @@ int plan_strips(df_handle *h)
     if (const char *e = std::getenv("DFAMD_ABLATE_HANDOFF")) h->ablate_handoff = std::atoi(e);
     h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
-    h->ypre = 0;
-    if (const char *e = std::getenv("DFAMD_YPRE")) h->ypre = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YLDS")) h->ylds = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_K3A_FAST")) h->k3a_fast = std::atoi(e);
     const int Ny = s.Ny;
@@ -1166,12 +1103,8 @@ int plan_rng(df_handle *h)
         // ceil(2^64 / W): floor(p * inv / 2^64) == p / W for every p < 2^32
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
-    g.gen_compact = 1;
-    g.dense_g = 8;
-    g.count_grid = 0;
     g.fast_log = 2; // glibc's own log in the polar transform: normals bit-identical (tests/test_rng_log.py)
     if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_GEN_COMPACT")) g.gen_compact = std::atoi(e);
     g.nt_stores = 1; // noise written past the caches: it is read once, by the next call's sweeps (A/B -1.4%)
     const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
     g.next_mult = next.mult;
@@ -1650,7 +1583,6 @@ int build(df_handle *h, const df_config_c *cfg)
             h->hb = cells <= (1ll << 16) || (nymax >= 128 && cells <= (1ll << 20)) ? 4 : cells <= (1ll << 20) ? 2 : 1;
     }
     if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_HB_BURST")) h->hb_burst = std::atoi(e);
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
     h->hb_conf = h->hb;
@@ -1676,7 +1608,7 @@ int step0(df_handle *h)
     int rc;
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
-    if ((rc = ypass_unless_done(h))) return rc;
+    if ((rc = phase_ypass(h, 7))) return rc;
     if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
     if ((rc = sync_all(h))) return rc;
@@ -1702,10 +1634,6 @@ void destroy(df_handle *h)
     if (h->comm) ncclCommDestroy(h->comm);
     if (h->ev_counted) (void)hipEventDestroy(h->ev_counted);
     if (h->ev_halo) (void)hipEventDestroy(h->ev_halo);
-    for (auto &g : h->graph)
-        if (g) (void)hipGraphExecDestroy(g);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
     for (int set = 0; set < 2; ++set) {
         if (h->ev_rng[set]) (void)hipEventDestroy(h->ev_rng[set]);
         if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
@@ -1721,95 +1649,6 @@ void destroy(df_handle *h)
 
 // Strips of one plane held by handles of this process: each phase runs on every
 // handle before the halo copies, then the z-pass. corr_sra = false is step 0.
-void drop_graphs(df_handle *h)
-{
-    for (auto &g : h->graph)
-        if (g) {
-            (void)hipGraphExecDestroy(g);
-            g = nullptr;
-        }
-}
-
-// The graph path applies to the steady state of a single-GPU handle: next call's noise already
-// enqueued, no per-call events (profiling), no CSV, no RCCL.
-bool graph_ok(df_handle *h)
-{
-    return h->use_graph && !h->ypre && h->hb == 1 && h->nsets == 2 && h->overlap && h->world == 1 && !h->group && !h->profiling &&
-           !h->halo_loopback && h->csv_path.empty() && h->gen_launched == h->gen_used + 1;
-}
-
-// Capture one call for noise set `cur`: sweeps on stream, the next generation (into set cur^1,
-// state slot cur^1 -> cur) on rng_stream, forked from and joined back to stream.
-int capture_call(df_handle *h, int cur, double dt, hipGraphExec_t *out)
-{
-    if (!h->ev_fork) HIP_OR(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), DF_EHIP);
-    if (!h->ev_join) HIP_OR(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), DF_EHIP);
-    HIP_OR(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal), DF_EHIP);
-    int rc = DF_OK;
-    const int saved_cur = h->cur;
-    auto body = [&]() -> int {
-        HIP_OR(hipEventRecord(h->ev_fork, h->stream), DF_EHIP);
-        HIP_OR(hipStreamWaitEvent(h->rng_stream, h->ev_fork, 0), DF_EHIP);
-        h->cur = cur;
-        int r;
-        if ((r = phase_ypass(h, 7))) return r;
-        if ((r = phase_zpass(h, true, true, dt))) return r;
-        const int nxt = cur ^ 1;
-        RngGeom g = h->geom;
-        for (int c = 0; c < 3; ++c) {
-            g.ry[c] = h->c[c].ry[nxt];
-            g.rz[c] = h->c[c].rz[nxt];
-        }
-        HIP_OR(launch_rng_count(g, h->rstate + nxt, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks,
-                                h->rng_blocks, h->rng_stream),
-               DF_EHIP);
-        HIP_OR(launch_rng_finish(g, h->rstate + nxt, h->rstate + cur, h->counts, h->wave_counts, h->offsets,
-                                 h->part, h->masks, h->tasks, h->ntasks, h->err_dev, h->rng_blocks, h->rng_blocks,
-                                 h->rng_stream),
-               DF_EHIP);
-        HIP_OR(hipEventRecord(h->ev_join, h->rng_stream), DF_EHIP);
-        HIP_OR(hipStreamWaitEvent(h->stream, h->ev_join, 0), DF_EHIP);
-        return DF_OK;
-    };
-    rc = body();
-    h->cur = saved_cur;
-    hipGraph_t graph = nullptr;
-    const hipError_t e = hipStreamEndCapture(h->stream, &graph); // always leave capture mode
-    if (rc) {
-        if (graph) (void)hipGraphDestroy(graph);
-        return rc;
-    }
-    if (e != hipSuccess) return fail(DF_EHIP, std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-    const hipError_t ei = hipGraphInstantiate(out, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) return fail(DF_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
-    return DF_OK;
-}
-
-// df_filter's steady state as one graph launch; bookkeeping mirrors consume_gen + prefetch_gen.
-int graph_call(df_handle *h, double dt)
-{
-    if (h->gen_used > 0) HIP_OR(hipEventRecord(h->ev_release[h->cur], h->stream), DF_EHIP);
-    const int cur = (int)(h->gen_used & 1);
-    HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[cur], 0), DF_EHIP); // this call's noise (maybe non-graph)
-    hipGraphExec_t &g = h->graph[cur];
-    if (g && h->graph_dt[cur] != dt) {
-        (void)hipGraphExecDestroy(g);
-        g = nullptr;
-    }
-    if (!g) {
-        int rc = capture_call(h, cur, dt, &g);
-        if (rc) return rc;
-        h->graph_dt[cur] = dt;
-    }
-    h->cur = cur;
-    h->gen_used++;
-    HIP_OR(hipGraphLaunch(g, h->stream), DF_EHIP);
-    HIP_OR(hipEventRecord(h->ev_rng[cur ^ 1], h->stream), DF_EHIP); // next call's noise is ready with the graph
-    h->gen_launched++;
-    return DF_OK;
-}
-
 int group_step(df_handle **hs, int n, bool corr_sra, double dt)
 {
     if (!hs || n < 1) return fail(DF_EINVAL, "empty handle group");
@@ -1958,7 +1797,6 @@ int df_filter(df_handle *h, double dt)
     if (h->hb != h->hb_conf && ++h->calls_since_load > kHbRestoreCalls) { // no state loads lately: batch again
         if ((rc = sync_all(h)) || (rc = restart_pipeline(h, h->hb_conf))) return rc;
     }
-    if (graph_ok(h)) return graph_call(h, dt);
     // Sampled phase events: each hipEventRecord is a queue packet between this call's kernels, and on
     // short calls six of them cost up to 10% of the call (tools/event_cost.py; profiles/r3/d)
     h->prof_call = h->profiling && (h->prof_seq++ % h->profile_every) == 0;
@@ -1966,7 +1804,7 @@ int df_filter(df_handle *h, double dt)
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
     ev_record(h, 0);
-    if ((rc = ypass_unless_done(h))) return rc;
+    if ((rc = phase_ypass(h, 7))) return rc;
     ev_record(h, 1);
     if ((rc = phase_halo_zpass(h, true, true, dt))) return rc; // phase event 2 inside
     ev_record(h, 3);
@@ -2298,8 +2136,8 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"zunroll", h->zunroll},
-        {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ycoop_map", h->ycoop_map}, {"ydepth", h->ydepth},
-        {"ylds", h->ylds}, {"ypre", h->ypre}, {"zocc", h->zocc}, {"handoff_batch", h->hb_conf},
+        {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ydepth", h->ydepth},
+        {"ylds", h->ylds}, {"handoff_batch", h->hb_conf},
         {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"fused_exchange", h->fused_x}, {"k3a_fast", h->k3a_fast}};
     for (const auto &kv : keys)
         if (k == kv.first) {
@@ -2319,15 +2157,14 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value != 1 && value != 2 && value != 4 && value != 8)
             return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");
         h->rows_per_wave = value;
-    } else if (k == "nt_loads") h->nt_loads = value != 0;
-    else if (k == "heavy_first") h->heavy_first = value != 0;
-    else if (k == "yunroll") h->yunroll = value >= 32 ? 32 : value >= 16 ? 16 : value >= 8 ? 8 : value >= 4 ? 4 : 2;
+    }
+    else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = h->ynt_stores = value != 0;
     else if (k == "znt_stores") h->nt_stores = value != 0;
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
-    else if (k == "zstage") h->zstage = value < 0 ? 0 : (value > 2 ? 2 : value);
-    else if (k == "ywindow") h->ywindow = value != 0;
+    else if (k == "zstage") h->zstage = value ? 2 : 0; // the element copy (1) is only the unaligned fallback now
+    else if (k == "ywindow") h->ywindow = value != 0; // shared y-pass kernel, table mode (ydepth 0)
     else if (k == "ydeep") h->ydeep = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
     else if (k == "ycoop_ovh") {
@@ -2341,24 +2178,16 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             }
         }
     }
-    else if (k == "ypre") h->ypre = value != 0; // from the next generation enqueued on
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on
-    else if (k == "zocc") h->zocc = value >= 8 ? 8 : 0;
     else if (k == "ydepth") h->ydepth = value < 0 ? 0 : value > 2 ? 2 : value;
-    else if (k == "ylds") h->ylds = value < 0 ? 0 : value > 3 ? 3 : value; // noise chunks in flight (0: off)
-    else if (k == "ylds_nw") h->ylds_nw = value == 8 ? 8 : 4;
-    else if (k == "ylds_ch") h->ylds_ch = value == 32 ? 32 : 16;
+    else if (k == "ylds") h->ylds = value ? 2 : 0; // LDS-staged table y-pass (2: two chunks in flight; 0: off)
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
         h->halo_overlap = value < 0 ? -1 : value != 0;
     }
 
-    else if (k == "ycoop_map") {
-        if (value != 0 && value != 1) return fail(DF_EINVAL, "ycoop_map must be 0 or 1");
-        h->ycoop_map = value;
-    }
     else if (k == "ycoop_order") {
         if (value < 0) return fail(DF_EINVAL, "ycoop_order must be >= 0");
         h->ycoop_order = value;
@@ -2371,10 +2200,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         }
     }
     else if (k == "ycoop") {
-        if (value < 0 || value > 8 || value == 5 || value == 6)
-            return fail(DF_EINVAL, "ycoop must be 0 or 1, 2, 3 (16, 8, 4 taps per wave per chunk), "
-                                   "4 (8 with the next chunk's loads in flight), "
-                                   "7, 8 (row pairs, 4 or 8 noise rows per wave per chunk)");
+        if (value != 0 && value != 7)
+            return fail(DF_EINVAL, "ycoop must be 0 (a wave per tile) or 7 (a block per row pair, 4 noise rows per "
+                                   "wave per chunk)");
         h->ycoop = value;
     }
     else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter
@@ -2390,7 +2218,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->halo_loopback = value;
     }
     else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
-    else if (k == "gen_compact") h->geom.gen_compact = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
@@ -2407,15 +2234,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             if ((rc = restart_pipeline(h, value))) return rc;
         } else h->hb = value;
     }
-    else if (k == "count_grid") {
-        if (value < 0) return fail(DF_EINVAL, "count_grid must be >= 0");
-        h->geom.count_grid = value;
-    }
-    else if (k == "dense_g") {
-        if (value != 4 && value != 8 && value != 16 && value != 32 && value != 128)
-            return fail(DF_EINVAL, "dense_g must be 4, 8, 16, 32 or 128");
-        h->geom.dense_g = value;
-    }
     else if (k == "gen_dense") {
         if (value && h->device >= 0 && !h->geom.cstate) {
             int rc = alloc_dense(h);
@@ -2428,7 +2246,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value < 0 || value > 2) return fail(DF_EINVAL, "fast_log must be 0 (device log), 1 (log_r2) or 2 (glibc_log)");
         h->geom.fast_log = value;
     }
-    else if (k == "graph") h->use_graph = value != 0;
     else if (k == "ywin_T" || k == "zwin_T") {
         if (value < 0 || value > (1 << 24) || (value & (value - 1)))
             return fail(DF_EINVAL, k + " must be 0 or a power of two <= 2^24 (ticks of the 100 MHz clock)");
@@ -2443,7 +2260,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->geom.gen_split = value;
     }
     else return fail(DF_EINVAL, "unknown tuning key: " + k);
-    drop_graphs(h); // captured launches carry the old shapes
     return DF_OK;
 }
 

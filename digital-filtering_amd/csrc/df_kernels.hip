@@ -145,7 +145,7 @@ __device__ __forceinline__ uint32_t lane_accept_bits(const RngGeom &g, uint64_t 
 
 // Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
 // the last z-strip rank's share) report zero.
-// Blocks [b0, b0 + nb) with a grid of gridDim.x <= nb blocks striding over them (RngGeom::count_grid
+// Blocks [b0, b0 + nb) of the call, one workgroup each (the loop strides only if a grid smaller than nb
 // caps how many K1 waves are resident beside the sweeps; 0 = one block per attempt block).
 __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                int *__restrict__ counts, int *__restrict__ wave_counts,
@@ -409,142 +409,9 @@ __global__ __launch_bounds__(256) void rng_plan_kernel(RngGeom g, const RngState
     }
 }
 
-// K3: one wave per task. Ranks come from K1's accept flags, so an attempt's draws are recomputed
-// only when one of its normals is stored (or it ends the call); every other attempt just jumps
-// the state to the lane's next attempt. Slots beyond the task count exit at once.
-__global__ __launch_bounds__(kRngThreads) void rng_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                                  RngStateDev *__restrict__ sout,
-                                                                  const WaveTask *__restrict__ tasks,
-                                                                  const int *__restrict__ ntasks,
-                                                                  const uint16_t *__restrict__ masks)
-{
-    const int lane = threadIdx.x & 63;
-    const int split = g.gen_split; // power of two <= kRngPerThread
-    const int vslot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
-    const int slot = vslot / split, sub = vslot - slot * split;
-    if (slot >= *ntasks) return;
-    const int gw = uniform(tasks[slot].gw);
-    long long rank_w = tasks[slot].r_lo; // uniform
-    const int b = gw / (kRngThreads / 64), tid = (gw % (kRngThreads / 64)) * 64 + lane;
-    // split counting: only counts were exchanged, so the flags of another rank's blocks are recomputed
-    const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    uint64_t st = thread_first_state(g, sin->state, b, tid); // start of attempt m
-    // This wave runs iterations [m0, m1) of the attempt wave: the state jumps over the first m0
-    // attempts of the lane and the rank over the whole wave's accepts among them.
-    const int per = kRngPerThread / split, m0 = sub * per, m1 = m0 + per;
-    for (int m = 0; m < m0; ++m) {
-        st = g.next_mult * st + g.next_plus;
-        rank_w += __popcll(__ballot((bits >> m) & 1u));
-    }
-    // The wave's runs of iterations m, m+1, ... are consecutive in the stream (wave-major ranks),
-    // so its position is located once and then advanced by 2*n_acc per iteration.
-    StreamPos P = stream_pos(g, f + 2ull * (uint64_t)rank_w);
-    for (int m = m0; m < m1; ++m) {
-        const bool acc = (bits >> m) & 1u;
-        const uint64_t mask = __ballot(acc);
-        // The wave's accepted attempts own the contiguous positions
-        // [q_first, q_first + 2*n_acc): locate q_first once per wave; a lane's
-        // position is then q_first + 2*below, at most one row wrap away when
-        // the run stays inside one array and rows hold >= 128 normals.
-        const int n_acc = __popcll(mask);
-        const long long rank0 = rank_w; // the wave's first rank in this iteration (uniform)
-        rank_w += n_acc;
-        const uint64_t q_first = f + 2ull * (uint64_t)rank0;
-        const StreamPos P0 = P; // == stream_pos(g, q_first)
-        P = stream_advance(g, P, 2u * (uint32_t)n_acc);
-        const int su = uniform(P0.sidx < 6 ? P0.sidx : 5);
-        // the run [q_first, q_first + 2*n_acc) stays inside array su (counts fit 32 bits: host check)
-        const uint32_t left = (g.rows[su] - P0.row) * g.width[su] - P0.col;
-        const bool fast = n_acc > 0 && P0.sidx < 6 && g.width[su] >= 2 * 64 && 2u * (uint32_t)n_acc <= left;
-        // Wave-uniform skip (SALU): the run [q_first, q_end) stays in one row of one array and
-        // every column it covers is one this GPU never stores (the r_zs interior, df.cpp:377,
-        // or another strip's r_ys columns), and it does not hold the call's last attempt.
-        bool idle = n_acc == 0;
-        if (fast && !(rank0 <= A - 1 && A - 1 < rank0 + n_acc)) {
-            const uint32_t c0 = P0.col, c1 = P0.col + 2u * (uint32_t)n_acc, W = g.width[su];
-            if (c1 <= W) {
-                if (su & 1) {
-                    const uint32_t nzp = (uint32_t)g.Nzp[su >> 1];
-                    idle = (!g.is_first || c0 >= nzp) && (!g.is_last || c1 <= nzp + (uint32_t)g.Nz_g);
-                } else {
-                    idle = c1 <= (uint32_t)g.z0 || c0 >= (uint32_t)g.z1;
-                }
-            }
-        }
-        if (idle) {
-            st = g.next_mult * st + g.next_plus;
-            continue;
-        }
-        if (acc) {
-            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            const long long rank = rank0 + below;
-            if (rank < A) {
-                const uint64_t q0 = q_first + 2ull * (uint64_t)below;
-                double *d0, *d1;
-                if (fast) { // one array, at most one row wrap: uniform array index, scalar tables
-                    const uint32_t W = g.width[su];
-                    StreamPos p0 = {su, P0.row, P0.col + 2u * (uint32_t)below};
-                    if (p0.col >= W) {
-                        p0.col -= W;
-                        p0.row++;
-                    }
-                    StreamPos p1 = {su, p0.row, p0.col + 1u}; // q0 + 1 < q_end <= end of array su
-                    if (p1.col == W) {
-                        p1.col = 0;
-                        p1.row++;
-                    }
-                    d0 = stream_dest(g, p0);
-                    d1 = stream_dest(g, p1);
-                } else {
-                    const StreamPos p0 = stream_pos(g, q0); // rare: per-lane table lookups
-                    d0 = stream_dest(g, p0);
-                    d1 = (q0 + 1 < g.Q) ? stream_dest(g, stream_next(g, p0)) : nullptr;
-                }
-                const bool last = (rank == A - 1);
-                if (d0 || d1 || last) {
-                    uint64_t s4 = st;
-                    PolarAttempt a;
-                    if (g.debug_flags & 4) {
-                        a.x = (double)(uint32_t)st * 1e-10;
-                        a.y = 0.5;
-                        a.r2 = 0.5;
-                        s4 = st + 4;
-                    } else {
-                        a = polar_attempt(s4); // same draws K1 tested
-                    }
-                    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * polar_log(g, a.r2) / a.r2);
-                    const double xm = a.x * mult;
-                    const double ym = a.y * mult;
-                    const double n0 = ym * 1.0 + 0.0, n1 = xm * 1.0 + 0.0;
-                    if (g.debug_flags & 2) {
-                        if (n0 == 1234.5) *d0 = n1; // keep the values alive
-                    } else if (d0 && d1 == d0 + 1 && ((uintptr_t)d0 & 15) == 0) {
-                        // adjacent and aligned (the common case): accepted lanes of a
-                        // wave then store one contiguous run of 16-B pairs
-                        if (g.nt_stores) __builtin_nontemporal_store(dvec2{n0, n1}, reinterpret_cast<dvec2 *>(d0));
-                        else *reinterpret_cast<double2 *>(d0) = make_double2(n0, n1);
-                    } else {
-                        if (d0) *d0 = n0;
-                        if (d1) *d1 = n1;
-                    }
-                    if (last) {
-                        sout->state = s4; // state after this attempt's 4th output
-                        sout->saved_flag = (int)((g.Q - f) & 1u);
-                        sout->saved = xm;
-                    }
-                }
-            }
-        }
-        st = g.next_mult * st + g.next_plus;
-    }
-}
-
-// K3, compacted form (the default; RngGeom::gen_compact). The sequential form above runs the
+// K3, compacted form (planes without the dense generation). A sequential form (round 1) ran the
 // transform (4 draws, log, sqrt, divide) in every iteration with the ~21% rejected lanes idle, and
-// walks the stream position per iteration in scalar code. Here a wave first appends the state of each
+// walked the stream position per iteration in scalar code. Here a wave first appends the state of each
 // accepted attempt to a wave-private LDS ring, in rank order (slot k = the wave's k-th accepted attempt,
 // stream positions q0 + 2k and q0 + 2k + 1), and every 4 iterations turns each full run of 64 slots into
 // one batch with all 64 lanes busy. A batch covers 128 consecutive stream positions, so whether it stores
@@ -1008,7 +875,9 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
     }
 }
 
-template <int kDenseG> // chunks per K3a wave (RngGeom::dense_g: 4, 8 or 16)
+// K3a: kDenseG needed chunks per wave (8; 4-128 measured alike, profiles/r3/e)
+constexpr int kDenseChunks = 8;
+template <int kDenseG>
 __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                         RngStateDev *__restrict__ sout)
 {
@@ -1318,8 +1187,7 @@ hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share,
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
-    const int grid = g.count_grid > 0 && g.count_grid < nb ? g.count_grid : nb;
-    hipLaunchKernelGGL(rng_count_kernel, dim3(grid), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
+    hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
                        nb, nb_total);
     return hipGetLastError();
 }
@@ -1351,20 +1219,12 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_dense_compact_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, offsets, part,
                            wave_counts, masks, nb_total);
         const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
-        const int per_block = g.dense_g * (kRngThreads / 64);
+        const int per_block = kDenseChunks * (kRngThreads / 64);
         const dim3 grid((nch + per_block - 1) / per_block);
-        switch (g.dense_g) {
-        case 4: hipLaunchKernelGGL(rng_dense_generate_kernel<4>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
-        case 16: hipLaunchKernelGGL(rng_dense_generate_kernel<16>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
-        case 32: hipLaunchKernelGGL(rng_dense_generate_kernel<32>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out); break;
-        case 128:
-            hipLaunchKernelGGL(rng_dense_generate_kernel<128>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
-            break;
-        default: hipLaunchKernelGGL(rng_dense_generate_kernel<8>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
-        }
+        hipLaunchKernelGGL(rng_dense_generate_kernel<kDenseChunks>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
         return hipGetLastError();
     }
-    if (g.fused_plan && g.gen_compact) {
+    if (g.fused_plan) {
         // the compacted K3 plans its own waves (small planes: one launch fewer per call)
     } else if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {
         hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
@@ -1376,12 +1236,8 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part,
                            wave_counts, nb_total, tasks, ntasks);
     }
-    if (g.gen_compact)
-        hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g,
-                           st_in, st_out, tasks, ntasks, masks, counts, wave_counts, err);
-    else
-        hipLaunchKernelGGL(rng_generate_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g, st_in,
-                           st_out, tasks, ntasks, masks);
+    hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g,
+                       st_in, st_out, tasks, ntasks, masks, counts, wave_counts, err);
     return hipGetLastError();
 }
 
@@ -1430,7 +1286,7 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
     if (tile >= a.nstrips * nrowblk) return;
     const int s = tile / nrowblk;          // strip-major: neighbouring tiles share noise rows
     int rb = tile - s * nrowblk;
-    if (a.heavy_first) rb = nrowblk - 1 - rb; // wide stencils (large j) start first: shorter tail
+    rb = nrowblk - 1 - rb; // wide stencils (large j) start first: shorter tail
     const int j0 = rb * R;
     const int Ny = a.Ny;
     const int nr = min(R, Ny - j0);
@@ -2011,78 +1867,6 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
     }
 }
 
-// K4, block-cooperative form for long tap chains (packed mode; SweepArgs::ycoop). One BLOCK per
-// (strip, row) tile instead of one wave: the tile's 2N+1 taps go in chunks of 4*KPW; wave w loads taps
-// w, w+4, ... of the chunk (KPW coefficient and noise pairs in flight per wave, 4*KPW per tile), writes
-// the products b*n to LDS, and after a barrier thread k < 128 adds cell k's products in tap order.
-// Every product and every addition is the one the per-wave kernel performs, in the same order
-// i = -N..N: bit-identical. On the reference's own grid (N_y up to 212, ~6 tiles per SIMD) a wave's
-// serial chain of 2N+1 dependent load rounds, not HBM bandwidth, set the per-wave kernel's time.
-// PIPE: the next chunk's loads are issued as soon as this chunk's products are in LDS, so they are in
-// flight through the barrier and the tap-order sum instead of after it (the barrier waits on LDS only).
-template <bool NT, int KPW, bool PIPE = false>
-__global__ __launch_bounds__(256) void ypass_coop_kernel(SweepArgs a)
-{
-    constexpr int CH = 4 * KPW; // taps per chunk
-    __shared__ double2 prod[CH][kStrip / 2];
-    const int c = blockIdx.y;
-    if (!((a.comps_mask >> c) & 1)) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int Ny = a.Ny;
-    const int per_xcd = gridDim.x >> 3; // XCD-aware order, as ypass_kernel
-    const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-    if (tile >= a.nstrips * Ny) return; // block-uniform
-    // rows in ascending order whatever heavy_first says: consecutive tiles of one XCD then share their
-    // noise rows in L2 (measured on the reference's grid: -8% against reversed rows, -18% against rows
-    // sorted by falling N; profiles/r2/ab_ycoop_native.jsonl)
-    const int s = tile / Ny;
-    const int j = tile - s * Ny;
-    const int N = a.Ny_st[c][(size_t)s * Ny + j];
-    const int T = 2 * N + 1;
-    const int col = s * kStrip + 2 * lane;
-    const bool live = col < a.Nz_loc;
-    const double *bp = a.By[c] + a.byoff[c][(size_t)s * Ny + j] + 2 * lane;       // tap t at bp + t*128
-    const double *np = a.ry[c] + (size_t)(j + a.Nyp[c] - N) * a.Pz + col;          // tap t at np + t*Pz
-    double acc = 0.0; // thread k < 128: cell s*128 + k
-    double2 b[KPW], n[KPW];
-    auto load = [&](int t0) {
-#pragma unroll
-        for (int k = 0; k < KPW; ++k) {
-            const int t = t0 + w + 4 * k;
-            if (live && t < T) {
-                b[k] = ldB<NT>(bp + (ptrdiff_t)t * kStrip);
-                n[k] = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * a.Pz), t);
-            } else {
-                b[k] = n[k] = make_double2(0.0, 0.0);
-            }
-        }
-    };
-    if (PIPE) load(0);
-    for (int t0 = 0; t0 < T; t0 += CH) {
-        if (!PIPE) load(t0);
-#pragma unroll
-        for (int k = 0; k < KPW; ++k) prod[w + 4 * k][lane] = make_double2(b[k].x * n[k].x, b[k].y * n[k].y);
-        if (PIPE && t0 + CH < T) load(t0 + CH); // block-uniform condition
-        __syncthreads();
-        if (threadIdx.x < kStrip) {
-            const double *pc = reinterpret_cast<const double *>(&prod[0][0]) + threadIdx.x;
-#if defined(DF_ABLATE_COOPSUM)
-            acc += pc[0]; // timing only: one product per chunk
-#else
-            const int nt = min(CH, T - t0);
-            for (int u = 0; u < nt; ++u) acc += pc[u * kStrip];
-#endif
-        }
-        __syncthreads();
-    }
-    const int k = s * kStrip + (int)threadIdx.x;
-    if (threadIdx.x < kStrip && k < a.Nz_loc) {
-        double *o = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c] + k;
-        if (a.ynt_stores) __builtin_nontemporal_store(acc, o);
-        else *o = acc;
-    }
-}
-
 // K4, block-cooperative form over a PAIR of rows (SweepArgs::ycoop 7, 8; 7 is the default for long
 // chains): one block per (strip, rows j0, j0 + 1). The block walks the union of the two rows' noise
 // ranges in chunks; wave w loads noise rows w, w+4, ... of the chunk once and both rows' coefficients
@@ -2109,14 +1893,8 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int Ny = a.Ny, nrowblk = (Ny + RR - 1) / RR;
     const int x = blockIdx.x & 7;
-    int pos;
-    if (a.ycoop2_map == 1) { // interleaved: tile t on XCD t % 8, no empty blocks
-        pos = (int)blockIdx.x;
-        if (pos >= a.nstrips * nrowblk) return;
-    } else {
-        pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
-        if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
-    }
+    const int pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
+    if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
 #if defined(DF_COOP2_ONLY_XCD)
     if (x != DF_COOP2_ONLY_XCD) return; // timing only: one XCD's run alone
 #endif
@@ -2259,8 +2037,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
     const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
     if (tile >= a.nstrips * nrowblk) return; // block-uniform
     const int s = tile / nrowblk;
-    int rb = tile - s * nrowblk;
-    if (a.heavy_first) rb = nrowblk - 1 - rb;
+    const int rb = nrowblk - 1 - (tile - s * nrowblk); // wide stencils first
     const int Ny = a.Ny, RB = NW * R, j0 = rb * RB;
     const int *nst = a.Ny_st[c] + (size_t)s * Ny;
     int mlo = 1 << 30, mhi = -(1 << 30); // the block's noise rows
@@ -2379,18 +2156,10 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 {
     if constexpr (TABLE) {
         if (a.ylds && !a.per_cell) {
-            if (a.ylds_nw == 8 && R == 1) { // timing variants: 8 rows per block, chunks of 16 or 32 noise rows
-                const int nrb8 = (a.Ny + 7) / 8;
-                const dim3 g8((unsigned)(((long long)a.nstrips * nrb8 + 7) / 8 * 8), 3);
-                if (a.ylds_ch == 32) hipLaunchKernelGGL((ypass_tlds_kernel<1, 2, 8, 32>), g8, dim3(512), 0, st, a, nrb8);
-                else hipLaunchKernelGGL((ypass_tlds_kernel<1, 2, 8, 16>), g8, dim3(512), 0, st, a, nrb8);
-                return hipGetLastError();
-            }
             const int nrowblk = (a.Ny + 4 * R - 1) / (4 * R);
             const unsigned blocks = (unsigned)(((long long)a.nstrips * nrowblk + 7) / 8 * 8);
             // 4 and 8 rows per wave take one chunk in flight: with 2-3 the compiler puts their arrays in scratch
-            if (R <= 2 && a.ylds >= 3) hipLaunchKernelGGL((ypass_tlds_kernel<R <= 2 ? R : 1, 3>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
-            else if (R <= 2 && a.ylds == 2) hipLaunchKernelGGL((ypass_tlds_kernel<R <= 2 ? R : 1, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
+            if (R <= 2) hipLaunchKernelGGL((ypass_tlds_kernel<R <= 2 ? R : 1, 2>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
             else hipLaunchKernelGGL((ypass_tlds_kernel<R, 1>), dim3(blocks, 3), dim3(256), 0, st, a, nrowblk);
             return hipGetLastError();
         }
@@ -2399,76 +2168,33 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle
     const dim3 grid(blocks, 3);
-    if (TABLE && a.per_cell)
-        hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
-    else if (TABLE && a.ydepth >= 1) { // ydepth 0: the shared ypass_kernel (A/B only)
-        constexpr int KYD = R <= 2 ? 4 : R == 4 ? 2 : 1;
-        if (a.ydepth >= 2 && R == 4) // timing: 3 groups ahead at 4 rows
-            hipLaunchKernelGGL((ypass_table_kernel<R, 3>), grid, dim3(256), 0, st, a, nrowblk);
-        else
-            hipLaunchKernelGGL((ypass_table_kernel<R, KYD>), grid, dim3(256), 0, st, a, nrowblk);
-    } else if (!TABLE && a.nt_loads) {
-        if constexpr (R <= 2) { // deeper rings (16 or 32 taps in flight) for one or two rows per wave
-            if (a.yunroll >= 32) {
-                hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 32, false>), grid, dim3(256), 0, st, a, nrowblk);
-                return hipGetLastError();
-            }
-            if (a.yunroll >= 16) {
-                hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 16, false>), grid, dim3(256), 0, st, a, nrowblk);
-                return hipGetLastError();
-            }
+    if constexpr (TABLE) {
+        if (a.per_cell) {
+            hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
+        } else if (a.ydepth >= 1) {
+            constexpr int KYD = R <= 2 ? 4 : R == 4 ? 2 : 1;
+            if (a.ydepth >= 2 && R == 4) // timing: 3 groups ahead at 4 rows
+                hipLaunchKernelGGL((ypass_table_kernel<R, 3>), grid, dim3(256), 0, st, a, nrowblk);
+            else
+                hipLaunchKernelGGL((ypass_table_kernel<R, KYD>), grid, dim3(256), 0, st, a, nrowblk);
+        } else { // ydepth 0: the shared ypass_kernel (A/B only)
+            hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
         }
-        if (a.yunroll >= 8)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
-        else if (a.yunroll >= 4)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
-        else
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, true, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
+    } else if (a.yunroll >= 8) {
+        hipLaunchKernelGGL((ypass_kernel<R, false, true, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
+    } else if (a.yunroll >= 4) {
+        hipLaunchKernelGGL((ypass_kernel<R, false, true, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
     } else {
-        if (a.yunroll >= 8)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
-        else if (a.yunroll >= 4)
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 4, false>), grid, dim3(256), 0, st, a, nrowblk);
-        else
-            hipLaunchKernelGGL((ypass_kernel<R, TABLE, false, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
+        hipLaunchKernelGGL((ypass_kernel<R, false, true, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
-    if (!table && a.ycoop >= 7) { // row pairs: 7 = 4 noise rows per wave per chunk (32 KiB LDS), 8 = 8 (64 KiB)
-        const unsigned tiles = (unsigned)(a.nstrips * ((a.Ny + 1) / 2));
-        const dim3 grid(a.ycoop2_map == 1 ? (tiles + 7) / 8 * 8 : (unsigned)(8 * a.ycoop2_run), 3);
-        if (a.ycoop == 7) {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop2_kernel<true, 4>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop2_kernel<false, 4>), grid, dim3(256), 0, st, a);
-        } else {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop2_kernel<true, 8>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop2_kernel<false, 8>), grid, dim3(256), 0, st, a);
-        }
-        return hipGetLastError();
-    }
-    if (!table && a.ycoop) {
-        const long long tiles = (long long)a.nstrips * a.Ny;
-        const dim3 grid((unsigned)((tiles + 7) / 8 * 8), 3);
-        // ycoop 1: 16 taps per wave per chunk (64 KiB of LDS, 2 blocks per CU); 2: 8 taps (32 KiB, 4 blocks);
-        // 3: 4 taps (16 KiB, 8 blocks)
-        // 4: 8 taps with the next chunk's loads in flight through the sum (PIPE; 5 and 6, the 4- and
-        // 16-tap forms, were measured slower and removed)
-        if (a.ycoop == 4) {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 8, true>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop_kernel<false, 8, true>), grid, dim3(256), 0, st, a);
-        } else if (a.ycoop >= 3) {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 4>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop_kernel<false, 4>), grid, dim3(256), 0, st, a);
-        } else if (a.ycoop == 2) {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 8>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop_kernel<false, 8>), grid, dim3(256), 0, st, a);
-        } else {
-            if (a.nt_loads) hipLaunchKernelGGL((ypass_coop_kernel<true, 16>), grid, dim3(256), 0, st, a);
-            else hipLaunchKernelGGL((ypass_coop_kernel<false, 16>), grid, dim3(256), 0, st, a);
-        }
+    if (!table && a.ycoop >= 7) { // row pairs, 4 noise rows per wave per chunk (32 KiB LDS)
+        const dim3 grid((unsigned)(8 * a.ycoop2_run), 3);
+        hipLaunchKernelGGL((ypass_coop2_kernel<true, 4>), grid, dim3(256), 0, st, a);
         return hipGetLastError();
     }
     switch (rows_per_wave) {
@@ -2537,10 +2263,8 @@ __device__ __forceinline__ void zstage_copy(const SweepArgs &a, double *lds, int
     }
 }
 
-// WPE: the register budget as waves per SIMD (amdgpu_waves_per_eu; 1 = the compiler's choice, 76 VGPRs and 6
-// waves here; 8 = 54-64 VGPRs, SweepArgs::zocc)
-template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false, int WPE = 1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void zpass_kernel(SweepArgs a)
+template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false>
+__global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
@@ -2550,7 +2274,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     int j = tile / nst;
     const int sl = tile - j * nst;
     const int s = a.zs_lo + sl + (sl >= a.zs_gap_at ? a.zs_gap : 0);
-    if (a.heavy_first) j = Ny - 1 - j;
+    j = Ny - 1 - j; // wide stencils first
     const int col = s * kStrip + 2 * lane;
 
     // Table mode, the block's 4 tiles on one row with one tap range per component: the
@@ -2780,22 +2504,14 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
         const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
-        if (u4 && a.zocc >= 8)
-            hipLaunchKernelGGL((zpass_kernel<true, false, 4, false, false, 8>), dim3(blocks), dim3(256), lds, st, a);
-        else if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
         else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
     } else if (a.zsplit) { // packed, one 3-wave block per tile
-        const unsigned b3 = (unsigned)tiles;
-        if (a.nt_loads) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<false, false, 4, false, true>), dim3(b3), dim3(192), 0, st, a);
-    } else if (a.nt_loads) {
-        if (u4 && a.zocc >= 8)
-            hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, false, 8>), dim3(blocks), dim3(256), 0, st, a);
-        else if (u4) hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3((unsigned)tiles), dim3(192), 0, st, a);
+    } else if (u4) {
+        hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
     } else {
-        if (u4) hipLaunchKernelGGL((zpass_kernel<false, false, 4, false>), dim3(blocks), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<false, false, 2, false>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);
     }
     return hipGetLastError();
 }

@@ -79,7 +79,6 @@ struct RngGeom {
     int nt_stores;                 // noise pairs stored non-temporally
     int gen_split;                 // K3 waves per attempt wave (1, 2, 4, 8, 16): each runs kRngPerThread/gen_split
                                    // iterations, so few-wave planes get short serial chains
-    int gen_compact;               // K3 form: 1 = accepted attempts compacted into full batches (default), 0 = sequential
     int fused_plan;                // compacted K3 plans its own waves (one GPU, nb_plan <= 1024 blocks): no K2/K2c launch
     int nb_plan;                   // attempt blocks of the call (fused_plan)
     int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
@@ -92,9 +91,7 @@ struct RngGeom {
     // Dense generation (gen_dense): Kc writes the start state of every accepted attempt whose 64-rank
     // chunk stores something here to cstate[rank]; K3a runs a wave per 8 such chunks (the host's list for
     // the call's parity f = incoming saved_flag), a lane per rank.
-    int gen_dense;
-    int dense_g;                    // needed chunks per K3a wave: 4, 8 (default), 16, 32, 128
-    int count_grid;                 // K1 blocks (striding over the attempt blocks); 0 = one per attempt block
+    int gen_dense;                  // 1: Kc + K3a; 2: run generation (K2s, K3r)
     uint64_t *cstate;               // [64 * chunk count]
     const uint32_t *need_bits[2];   // bitmap over chunks (+ 2 padding words), per parity f
     const uint32_t *chunks[2];      // needed chunk ids in increasing order, per parity f
@@ -140,29 +137,24 @@ struct SweepArgs {
     double sa[3], s1a[3];   // sqrt(alpha), sqrt(1-alpha) per component
     int do_corr, do_sra, comps_mask;
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
-    int nt_loads;           // non-temporal loads for the coefficient stream
-    int heavy_first;        // schedule rows with the widest stencils first
-    int yunroll, zunroll;   // taps per loop iteration (tuning knobs)
+    int yunroll, zunroll;   // taps per loop iteration: packed y 2, 4, 8 (deep ring); z 2, 4
     int nt_stores;          // z-pass outputs stored non-temporally
     int ynt_stores;         // y-pass output (r_zs) stored non-temporally
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS (2: 16-B copy,
                             // all loads issued before the stores)
     int zsplit;             // packed z-pass: one 3-wave block per tile, a wave per component (few tiles per SIMD)
-    int ycoop;              // packed y-pass: one block per (strip, row) tile, taps shared by 4 waves (long chains)
+    int ycoop;              // packed y-pass: 7 = one block per row pair (long chains), 0 = a wave per tile
     int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)
     int ycoop2_run;         // the longest such run (grid = 8 x this)
     const int *ycoop2_perm[3]; // dispatch position -> tile inside each run (nullptr: ascending)
-    int ycoop2_map;            // 0: XCD x runs tiles [ycoop2_xcd[c][x], ...); 1: tile t on XCD t % 8 (interleaved)
-    int zocc;                  // z-pass register budget: 0 the compiler's (6 waves per SIMD), 8 (8 waves, zpass WPE)
-    int ydepth;                // table y-pass at 1-2 rows per wave: noise 4 groups of 4 rows ahead (1) or 1-2 (0)
+    int ydepth;                // table y-pass: 1 ypass_table_kernel (2: 3 noise groups ahead at 4 rows); 0 the shared kernel
     int ylds;                  // table y-pass with the noise staged in LDS per block of 4R rows (ypass_tlds_kernel)
-    int ylds_nw, ylds_ch;      // its waves per block (4; 8 with one row each) and noise rows per chunk (16; 32)
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.
     int zs_lo, zs_n, zs_gap_at, zs_gap;
-    int ywindow;            // table y-pass: uniform-N tiles read one prefetched coefficient window per 4 taps
-    int ydeep;              // table y-pass: noise and coefficients loaded a whole 4-tap group ahead
+    int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
+    int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is
     // in the first W ticks of a T-tick period, so the CUs write together and the read stream runs

@@ -149,11 +149,16 @@ def test_c_abi_rejects_bad_arguments():
     native = host()  # the reference's grid: long y chains, the row-pair plan
     assert L.df_set_tuning(native._h, b"ycoop_ovh", 64) == 0
     # round-3 keys: the dispatch order re-plans device tables only on handles that have them
-    for key, val in ((b"ycoop_order", 4), (b"ycoop_order", 0), (b"ycoop_map", 1), (b"ypre", 1), (b"zocc", 8),
-                     (b"k3a_fast", 0), (b"ydepth", 0), (b"yunroll", 32), (b"halo_overlap", 0), (b"halo_overlap", -1)):
+    for key, val in ((b"ycoop_order", 4), (b"ycoop_order", 0), (b"k3a_fast", 0), (b"ydepth", 0), (b"yunroll", 8),
+                     (b"halo_overlap", 0), (b"halo_overlap", -1), (b"gen_dense", 2), (b"fused_exchange", 0)):
         assert L.df_set_tuning(native._h, key, val) == 0, key
     assert L.df_set_tuning(native._h, b"ycoop_order", -1) == -1
-    assert L.df_set_tuning(native._h, b"ycoop_map", 2) == -1
+    # round 4: variants measured neutral or slower are gone from the library, not just off
+    for key in (b"ycoop_map", b"ypre", b"zocc", b"graph", b"count_grid", b"dense_g", b"gen_compact", b"nt_loads",
+                b"heavy_first", b"ylds_nw", b"ylds_ch"):
+        assert L.df_set_tuning(native._h, key, 1) == -1, key
+        assert b"unknown tuning" in L.df_last_error()
+    assert L.df_set_tuning(native._h, b"ycoop", 3) == -1
     cfg, keep = dfamd.make_config(device=-1, seed=1, coeff_mode="packed")
     cfg.coeff_mode = 7
     assert not L.df_create(C.byref(cfg))

@@ -18,16 +18,14 @@ rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 7
 calls = int(sys.argv[4]) if len(sys.argv) > 4 else 48
 dims = {"c1": (128, 128, 8, 8), "c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64)}
 hs = {}
-for v in ("1", "2", "4", "2b", "4b"):  # "b": the epoch's generations in one burst (DFAMD_HB_BURST=1)
+for v in ("1", "2", "4"):
     os.environ["DFAMD_HANDOFF_BATCH"] = v.rstrip("b")
-    os.environ["DFAMD_HB_BURST"] = "1" if v.endswith("b") else "0"
     if cfg == "native":
         hs[v] = dfamd.DigitalFilter(seed=1, device=0, coeff_mode=mode)
     else:
         Ny, Nz, a, b = dims[cfg]
         hs[v] = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=a, N_max=b, seed=1, device=0, coeff_mode=mode)
 os.environ.pop("DFAMD_HANDOFF_BATCH")
-os.environ.pop("DFAMD_HB_BURST")
 res = {v: [] for v in hs}
 for f in hs.values():
     for _ in range(32):

@@ -323,6 +323,7 @@ SweepArgs sweep_args(df_handle *h)
     a.zs_lo = 0;
     a.zs_n = a.zs_gap_at = h->nstrips;
     a.zs_gap = 0;
+    a.zgroup = 1;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
     a.tabf = h->tabf;
@@ -817,6 +818,7 @@ int phase_zpass(df_handle *h, bool corr, bool sra, double dt, int part, hipStrea
             a.zs_gap_at = lo;
             a.zs_gap = hi - lo;
             a.zstage = 0; // a block's 4 tiles may straddle the gap
+            a.zgroup = 0;
         }
     }
     if (corr) {

@@ -2268,36 +2268,43 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
-    const int tile = SPLIT ? (int)blockIdx.x : uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int Ny = a.Ny, nst = a.zs_n; // this launch's strips (SweepArgs::zs_lo ...)
-    if (tile >= nst * Ny) return; // block-uniform when SPLIT
-    int j = tile / nst;
-    const int sl = tile - j * nst;
-    const int s = a.zs_lo + sl + (sl >= a.zs_gap_at ? a.zs_gap : 0);
-    j = Ny - 1 - j; // wide stencils first
-    const int col = s * kStrip + 2 * lane;
-
-    // Table mode, the block's 4 tiles on one row with one tap range per component: the
-    // block stages that row's noise (512 + 2N columns per component) in LDS once and
-    // the waves read their tap pairs from there (ds_read_b128) instead of 4 overlapping
-    // (128 + 2N)-column windows through L1. Block-uniform: the barrier is reached by all.
+    int j, s;
     bool staged = false;
-    if (TABLE && !PC && a.zstage) { // (launches with a strip gap run unstaged: zstage 0)
-        const int t0 = blockIdx.x * 4;
-        staged = t0 + 3 < nst * Ny && t0 / nst == (t0 + 3) / nst;
-        const int s0 = a.zs_lo + t0 - (t0 / nst) * nst;
+    if (TABLE && !PC && a.zgroup) {
+        // Table mode, launches without a strip gap: block = (row, group of <= 4 consecutive strips), wave w =
+        // strip 4 g + w, so no block straddles two rows (a z-strip rank's 6 interior strips per row are groups
+        // of 4 and 2, not blocks across rows). Where the group's strips share one tap range per component the
+        // block stages that row's noise (128 ns + 2N columns per component) in LDS once and the waves read
+        // their tap pairs from there (ds_read_b128) instead of overlapping (128 + 2N)-column windows through
+        // L1. Block-uniform: the barrier is reached by all; waves past the group leave after the copy.
+        const int ngrp = (nst + 3) >> 2;
+        const int jj = (int)blockIdx.x / ngrp, g = (int)blockIdx.x - jj * ngrp;
+        if (jj >= Ny) return; // block-uniform
+        j = Ny - 1 - jj;      // wide stencils first
+        const int s0 = a.zs_lo + 4 * g, ns = min(4, nst - 4 * g), w = uniform(threadIdx.x >> 6);
+        s = s0 + w;
+        staged = a.zstage != 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             if (!staged || !((a.comps_mask >> c) & 1)) continue;
-            const int *ns = a.Nz_st[c] + (size_t)s0 * Ny + j;
-            const int N0 = ns[0];
-            staged = ns[Ny] == N0 && ns[2 * Ny] == N0 && ns[3 * Ny] == N0;
+            const int *nz = a.Nz_st[c] + (size_t)s0 * Ny + j;
+            for (int k = 1; k < ns; ++k) staged = staged && nz[(size_t)k * Ny] == nz[0];
         }
         if (staged) {
-            zstage_copy(a, zstage_lds, j, s0, 4, 256);
+            zstage_copy(a, zstage_lds, j, s0, ns, 256);
             __syncthreads();
         }
+        if (w >= ns) return;
+    } else {
+        const int tile = SPLIT ? (int)blockIdx.x : uniform(blockIdx.x * 4 + (threadIdx.x >> 6));
+        if (tile >= nst * Ny) return; // block-uniform when SPLIT
+        const int jj = tile / nst;
+        const int sl = tile - jj * nst;
+        s = a.zs_lo + sl + (sl >= a.zs_gap_at ? a.zs_gap : 0);
+        j = Ny - 1 - jj; // wide stencils first
     }
+    const int col = s * kStrip + 2 * lane;
     // padding lanes leave (after their share of the staging copy); SPLIT keeps them to the barrier
     // (their loads stay inside the padded strip: B holds 128 cells per strip, r_zs Pz + 2 Nzp columns)
     if (!SPLIT && col >= a.Nz_loc) return;
@@ -2503,9 +2510,10 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
     if (table && a.per_cell) {
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
-        const size_t lds = a.zstage ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
-        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), dim3(blocks), dim3(256), lds, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), dim3(blocks), dim3(256), lds, st, a);
+        const size_t lds = a.zstage && a.zgroup ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
+        const dim3 grid(a.zgroup ? (unsigned)(a.Ny * ((a.zs_n + 3) / 4)) : blocks);
+        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), grid, dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), grid, dim3(256), lds, st, a);
     } else if (a.zsplit) { // packed, one 3-wave block per tile
         hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3((unsigned)tiles), dim3(192), 0, st, a);
     } else if (u4) {

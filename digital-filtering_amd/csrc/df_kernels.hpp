@@ -153,6 +153,7 @@ struct SweepArgs {
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.
     int zs_lo, zs_n, zs_gap_at, zs_gap;
+    int zgroup;             // table z-pass: blocks of (row, <= 4 consecutive strips) (launches without a gap)
     int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
     int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)

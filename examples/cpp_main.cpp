@@ -84,6 +84,55 @@ int main(int argc, char **argv)
         return 0;
     }
 
+    if (argc >= 2 && std::string(argv[1]) == "remirror") {
+        // the host mirrors are the public vectors (df.hpp:28, 59), page-locked by the wrapper. A
+        // caller may move, swap or re-allocate them between calls; every later refresh must land in the
+        // vector the caller holds then. Checked against a fresh df_get_field copy after each call.
+        config.plane = DF_PLANE_SYNTHETIC;
+        config.Ny = 96;
+        config.Nz = 300;
+        config.N_min = 2;
+        config.N_max = 12;
+        config.seed = 5;
+        config.seed_from_random_device = false;
+        config.verbose = false;
+        DIGITAL_FILTER df(config);
+        const size_t n = df.u.fluc.size();
+        int bad = 0;
+        auto check = [&](int step) {
+            const std::pair<Vector *, int> m[5] = {{&df.u.fluc, DF_U}, {&df.v.fluc, DF_V}, {&df.w.fluc, DF_W},
+                                                   {nullptr, DF_T}, {nullptr, DF_RHO}};
+            for (const auto &p : m) {
+                if (!p.first) continue;
+                Vector ref(n);
+                if (df_get_field(df.handle(), p.second, ref.data()) != DF_OK || *p.first != ref) {
+                    std::cerr << "mirror of field " << p.second << " stale after step " << step << std::endl;
+                    ++bad;
+                }
+            }
+        };
+        df.filter(1e-8);
+        check(0);
+        for (int step = 1; step <= 6; ++step) {
+            switch (step % 3) {
+            case 1: df.u.fluc = Vector(n, 7.0); break; // move-assign: a new buffer, the pinned one freed
+            case 2: {
+                Vector other(n, -3.0);
+                std::swap(df.v.fluc, other); // the pinned buffer now belongs to `other`, freed at scope end
+                break;
+            }
+            default:
+                df.w.fluc.clear(); // freed and re-allocated at the same size: often the same address
+                df.w.fluc.shrink_to_fit();
+                df.w.fluc.resize(n, 1.0);
+            }
+            df.filter(1e-8);
+            check(step);
+        }
+        std::cout << "remirror " << (bad ? "FAILED" : "ok") << " (" << bad << " stale mirrors)" << std::endl;
+        return bad ? 1 : 0;
+    }
+
     if (argc >= 10 && std::string(argv[1]) == "twin") {
         config.plane = DF_PLANE_SYNTHETIC;
         config.Ny = std::atoi(argv[2]);

@@ -127,3 +127,11 @@ def test_variance_invariant_over_time():
         assert np.all(np.abs(ratio - 1) < 0.08), (got, ratio.min(), ratio.max())
     cov = acc["uv"][rows] / n
     assert np.all(np.abs(cov - R["R21"][rows]) < 0.1 * np.sqrt(R["R11"][rows] * R["R22"][rows]))
+
+
+def test_cpp_mirrors_follow_moved_or_reallocated_vectors():
+    # u.fluc etc. are the caller's vectors, page-locked by the wrapper; moving, swapping or
+    # re-allocating them between filter() calls must not leave a stale or freed registration behind
+    out = subprocess.run([EXE, "remirror"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "remirror ok" in out.stdout

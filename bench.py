@@ -100,7 +100,7 @@ def parse(argv=None):
                    help="comma list of further configs timed after the main one, same mode and rule; "
                         "auto: 'native,c2' on one GPU, 'c5' on N > 1; '' for none")
     p.add_argument("--alt-modes", default="auto", choices=["auto", "off"],
-                   help="also time the other coefficient mode (N=1 only) and report it under alt_modes")
+                   help="also time the other coefficient mode (at N > 1 split the same way) and report it under alt_modes")
     p.add_argument("--same-plane", default="auto", choices=["auto", "off"],
                    help="N > 1: rank 0 also times the whole plane unsplit on its own GPU (same_plane_1gpu)")
     p.add_argument("--long-run", default="auto",
@@ -697,6 +697,27 @@ def main(argv=None):
     head = summarize(ctx, wl, args, recs)
 
     alt = None
+    if ctx.world > 1 and args.alt_modes == "auto":
+        # the other coefficient mode split the same way (table: the C/C++/Fortran drop-in default; split counting,
+        # run generation, group counts in the halo group), checked against the unsplit plane like the headline
+        other = "table" if args.coeff_mode == "packed" else "packed"
+        if ctx.rank == 0:
+            progress(f"{name}: {other} mode over {ctx.world} rank(s)")
+        saved_mode = args.coeff_mode
+        args.coeff_mode = other
+        try:
+            h2, arec = run_config(dfamd, ctx, wl, args, ctx.comm_id(dfamd))
+            asum = summarize(ctx, wl, args, ctx.gather(arec))
+            aps = ctx.gather(parity_check(dfamd, ctx, wl, args, h2, h2.calls_done)) if args.parity == "on" else None
+            acomm = h2.comm_info()
+            h2.close()
+        finally:
+            args.coeff_mode = saved_mode
+        ctx.barrier()
+        alt = {other: {"value": asum["value"], "ms_per_step": asum["ms_per_step"],
+                       "phase_ms_per_call": asum["phase_ms_per_call"], "multi_gpu": asum.get("multi_gpu"),
+                       "parity_ok": all(p["ok"] for p in aps) if aps else None,
+                       "rng_collective_bytes_per_call": acomm.get("rng_bytes_received")}}
     if ctx.world == 1 and args.alt_modes == "auto" and wl["plane"] != "native":
         other = "table" if args.coeff_mode == "packed" else "packed"
         g = make_filter(dfamd, ctx, wl, args, other)

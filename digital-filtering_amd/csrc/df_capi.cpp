@@ -1465,8 +1465,9 @@ int alloc_dense(df_handle *h)
         for (uint64_t c = 0; c < nch; ++c)
             if ((bits[f][c >> 5] >> (c & 31)) & 1u) list[f].push_back((uint32_t)c);
     }
-    // K3a fast chunks (one GPU): all 128 positions in one r_ys array (every column stored), at most one row wrap,
-    // every rank live and none the call's last (that one sets the stream state): destinations by arithmetic
+    // K3a / K3r fast chunks: all 128 positions in one r_ys array (one GPU: every column stored, at most one row
+    // wrap; a z-strip: inside the strip's columns of one row), every rank live and none the call's last (that one
+    // sets the stream state): destinations by arithmetic
     std::vector<ChunkDest> dest[2];
     for (int f = 0; f < 2; ++f) {
         const long long A = (long long)((g.Q - f + 1) / 2);
@@ -1477,12 +1478,19 @@ int alloc_dense(df_handle *h)
             int su = 0;
             while (su < 5 && q0 >= g.seg[su + 1]) ++su;
             const uint64_t W = g.width[su];
-            if ((su & 1) || g.z0 != 0 || g.z1 != g.Nz_g || W < 128 || q0 + 128 > g.seg[su + 1]) continue;
+            if ((su & 1) || W < 128 || q0 + 128 > g.seg[su + 1]) continue;
             const uint64_t p = q0 - g.seg[su], row = p / W, col = p % W;
             ChunkDest d{};
-            d.off = (long long)(row * (uint64_t)g.Pz + col);
-            d.wr = (short)std::min<uint64_t>(128, W - col);
-            d.jump = g.Pz - (int)W;
+            if (g.z0 == 0 && (uint64_t)g.z1 == W) { // every column stored: at most one row wrap
+                d.off = (long long)(row * (uint64_t)g.Pz + col);
+                d.wr = (short)std::min<uint64_t>(128, W - col);
+                d.jump = g.Pz - (int)W;
+            } else { // a z-strip: the chunk's 128 positions inside this strip's columns of one row (round 4)
+                if (col < (uint64_t)g.z0 || col + 128 > (uint64_t)g.z1) continue;
+                d.off = (long long)(row * (uint64_t)g.Pz + (col - (uint64_t)g.z0));
+                d.wr = 128;
+                d.jump = 0;
+            }
             d.arr = (signed char)su;
             dest[f][i] = d;
         }

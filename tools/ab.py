@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """In-process A/B timing of library variants on one GPU (guide §5.4 rule 24).
 
-    python3 tools/ab.py --a "DFAMD_HEAVY_FIRST=0" --b "DFAMD_HEAVY_FIRST=1" [--config c3] [--mode packed]
+    python3 tools/ab.py --a "DFAMD_GEN_DENSE=1" --b "DFAMD_GEN_DENSE=2" [--config c3] [--mode table]
 
 Each variant is a separate handle created with its env knobs set; the handles
 run interleaved rounds of K calls and the per-phase hipEvent times are reported

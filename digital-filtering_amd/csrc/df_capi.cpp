@@ -111,6 +111,7 @@ struct df_handle {
     // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
+    int zpipe = 0; // table z-pass software pipelining (SweepArgs::zpipe)
     int ablate_handoff = 0; // DFAMD_ABLATE_HANDOFF: timing-only ablation of the per-call stream hand-off
     int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
     // Dense generation (RngGeom::gen_dense: compaction through memory, one wave per needed 64-rank chunk,
@@ -324,6 +325,7 @@ SweepArgs sweep_args(df_handle *h)
     a.zs_n = a.zs_gap_at = h->nstrips;
     a.zs_gap = 0;
     a.zgroup = 1;
+    a.zpipe = h->zpipe;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
     a.tabf = h->tabf;
@@ -2174,6 +2176,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "znt_stores") h->nt_stores = value != 0;
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value ? 2 : 0; // the element copy (1) is only the unaligned fallback now
+    else if (k == "zpipe") h->zpipe = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0; // shared y-pass kernel, table mode (ydepth 0)
     else if (k == "ydeep") h->ydeep = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;

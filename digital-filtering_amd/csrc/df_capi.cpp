@@ -111,7 +111,6 @@ struct df_handle {
     // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
-    int zpipe = 0; // table z-pass software pipelining (SweepArgs::zpipe)
     int ablate_handoff = 0; // DFAMD_ABLATE_HANDOFF: timing-only ablation of the per-call stream hand-off
     int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
     // Dense generation (RngGeom::gen_dense: compaction through memory, one wave per needed 64-rank chunk,
@@ -325,7 +324,6 @@ SweepArgs sweep_args(df_handle *h)
     a.zs_n = a.zs_gap_at = h->nstrips;
     a.zs_gap = 0;
     a.zgroup = 1;
-    a.zpipe = h->zpipe;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
     a.tabf = h->tabf;
@@ -1040,7 +1038,11 @@ int plan_strips(df_handle *h)
     h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE || h->ycoop < 7 ? 1 : 0;
     if (const char *e = std::getenv("DFAMD_FUSE_PLAN")) h->fuse_plan = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_ABLATE_HANDOFF")) h->ablate_handoff = std::atoi(e);
-    h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 1 : 0;
+    // Table mode generates its noise through the run form (round 4: group counts, one wave per piece of needed
+    // chunks): with split counting it needs no pass over the whole stream after the exchange and its counts
+    // travel in the halo group (c4 over 8, one rank: 0.25-0.26 -> 0.24 ms per call, profiles/r4/d); on one GPU
+    // it is even with Kc + K3a (c3 0.364 vs 0.366 ms, profiles/r4/e).
+    h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 2 : 0;
     if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_YLDS")) h->ylds = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_K3A_FAST")) h->k3a_fast = std::atoi(e);
@@ -1593,6 +1595,10 @@ int build(df_handle *h, const df_config_c *cfg)
         const long long cells = (long long)h->Ny * h->Nz_loc;
         if (h->world == 1 && !cfg->comm_id)
             h->hb = cells <= (1ll << 16) || (nymax >= 128 && cells <= (1ll << 20)) ? 4 : cells <= (1ll << 20) ? 2 : 1;
+        // Table mode on larger single-GPU planes (round 4): its RNG chain competes for the same VALU slots as the
+        // sweeps and, with one generation per hand-off, ends up on the critical path; two generations per epoch
+        // let it run a call further ahead (c3: 0.366 -> 0.352 ms per call median, profiles/r4/e).
+        if (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb == 1) h->hb = 2;
     }
     if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
@@ -2176,7 +2182,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "znt_stores") h->nt_stores = value != 0;
     else if (k == "ynt_stores") h->ynt_stores = value != 0;
     else if (k == "zstage") h->zstage = value ? 2 : 0; // the element copy (1) is only the unaligned fallback now
-    else if (k == "zpipe") h->zpipe = value != 0;
     else if (k == "ywindow") h->ywindow = value != 0; // shared y-pass kernel, table mode (ydepth 0)
     else if (k == "ydeep") h->ydeep = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;

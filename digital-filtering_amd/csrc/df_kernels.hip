@@ -2399,89 +2399,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         r0 = acc0;
         r1 = acc1;
         };
-        if (TABLE && !PC && staged && a.zpipe) {
-            // Staged table path, software-pipelined (zpipe): the next 8 taps' noise pairs (ds_read_b128) and their
-            // coefficient window (one scalar load) are issued before this iteration's products, so the wait the
-            // shared LDS + scalar counter forces (lgkmcnt(0): scalar loads return out of order) lands a whole
-            // iteration after the issue instead of right after it. Same products, same order: bit-identical.
-            const lds_pair_ptr xp = (lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane);
-            double acc0 = 0.0, acc1 = 0.0;
-            double2 P = DF_NOISE(xp, 0);
-            int m = 0;
-            if (N >= 8) {
-                double2 Q1 = DF_NOISE(xp + 1, 1), Q2 = DF_NOISE(xp + 2, 2), Q3 = DF_NOISE(xp + 3, 3), Q4 = DF_NOISE(xp + 4, 4);
-                double w[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) w[u] = DF_TCOEF(tb[u]);
-                auto eight = [&](const double2 p0, const double2 q1, const double2 q2, const double2 q3, const double2 q4,
-                                 const double (&ww)[8]) {
-                    acc0 += ww[0] * p0.x;
-                    acc1 += ww[0] * p0.y;
-                    acc0 += ww[1] * p0.y;
-                    acc1 += ww[1] * q1.x;
-                    acc0 += ww[2] * q1.x;
-                    acc1 += ww[2] * q1.y;
-                    acc0 += ww[3] * q1.y;
-                    acc1 += ww[3] * q2.x;
-                    acc0 += ww[4] * q2.x;
-                    acc1 += ww[4] * q2.y;
-                    acc0 += ww[5] * q2.y;
-                    acc1 += ww[5] * q3.x;
-                    acc0 += ww[6] * q3.x;
-                    acc1 += ww[6] * q3.y;
-                    acc0 += ww[7] * q3.y;
-                    acc1 += ww[7] * q4.x;
-                };
-                for (; m + 8 <= N; m += 4) { // loads of iteration m + 4 stay within the stencil (m + 8 <= N)
-                    const double2 R1 = DF_NOISE(xp + m + 5, m + 5), R2 = DF_NOISE(xp + m + 6, m + 6),
-                                  R3 = DF_NOISE(xp + m + 7, m + 7), R4 = DF_NOISE(xp + m + 8, m + 8);
-                    double wn[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) wn[u] = DF_TCOEF(tb[2 * m + 8 + u]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    eight(P, Q1, Q2, Q3, Q4, w);
-                    __builtin_amdgcn_sched_barrier(0);
-                    P = Q4;
-                    Q1 = R1;
-                    Q2 = R2;
-                    Q3 = R3;
-                    Q4 = R4;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) w[u] = wn[u];
-                }
-                eight(P, Q1, Q2, Q3, Q4, w); // m + 4 <= N: the prefetched iteration
-                P = Q4;
-                m += 4;
-            }
-            for (; m + 2 <= N; m += 2) {
-                const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2);
-                const double b0 = DF_TCOEF(tb[2 * m]), b1 = DF_TCOEF(tb[2 * m + 1]), b2 = DF_TCOEF(tb[2 * m + 2]),
-                             b3 = DF_TCOEF(tb[2 * m + 3]);
-                acc0 += b0 * P.x;
-                acc1 += b0 * P.y;
-                acc0 += b1 * P.y;
-                acc1 += b1 * P1.x;
-                acc0 += b2 * P1.x;
-                acc1 += b2 * P1.y;
-                acc0 += b3 * P1.y;
-                acc1 += b3 * P2.x;
-                P = P2;
-            }
-            for (; m < N; ++m) {
-                const double2 P1 = DF_NOISE(xp + m + 1, m + 1);
-                const double b0 = DF_TCOEF(tb[2 * m]), b1 = DF_TCOEF(tb[2 * m + 1]);
-                acc0 += b0 * P.x;
-                acc1 += b0 * P.y;
-                acc0 += b1 * P.y;
-                acc1 += b1 * P1.x;
-                P = P1;
-            }
-            const double bl = DF_TCOEF(tb[2 * N]);
-            acc0 += bl * P.x;
-            acc1 += bl * P.y;
-            f0[c] = acc0;
-            f1[c] = acc1;
-        } else if (TABLE && !PC && staged) {
+        if (TABLE && !PC && staged) {
             taps((lds_pair_ptr)(zstage_lds + c * a.zstage_reg + (threadIdx.x >> 6) * kStrip + 2 * lane), f0[c], f1[c]);
         } else {
             taps(gxp, f0[c], f1[c]);

@@ -154,7 +154,6 @@ struct SweepArgs {
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.
     int zs_lo, zs_n, zs_gap_at, zs_gap;
     int zgroup;             // table z-pass: blocks of (row, <= 4 consecutive strips) (launches without a gap)
-    int zpipe;              // table z-pass, staged: the next 8 taps' loads issued before this iteration's products
     int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
     int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)

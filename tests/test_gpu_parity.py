@@ -307,7 +307,7 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
-                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(zpipe=1), dict(zpipe=1, zunroll=2), dict(zpipe=0)]
+                dict(ylds=1, rows_per_wave=8), dict(ylds=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)
@@ -423,11 +423,10 @@ def test_table_lds_staging_is_bitexact(spec):
 def test_table_zstage_copies_are_bitexact(spec):
     # the staging copies of the table z-pass (0 none; 1 and 2 both the 16-B copy with loads first):
     # full and partial groups of 4 strips (6, 9, 2 and 3 strips), odd and even Nz, against packed
-    hs = [gpu_synth(*spec, seed=8, coeff_mode="table") for _ in range(4)]
+    hs = [gpu_synth(*spec, seed=8, coeff_mode="table") for _ in range(3)]
     p = gpu_synth(*spec, seed=8, coeff_mode="packed")
-    for level, h in enumerate(hs[:3]):
+    for level, h in enumerate(hs):
         h.set_tuning("zstage", level)
-    hs[3].set_tuning("zpipe", 1)  # staged and software-pipelined
     for _ in range(3):
         for f in hs + [p]:
             f.filter(1e-8)

@@ -329,9 +329,10 @@ def test_alloc_registry_rejects_overlapping_ranges():
     # packed the row-pair y-pass in heaviest-first groups of 4
     (dict(), "table", dict(rows_per_wave=1, ylds=2, handoff_batch=4, ycoop=0)),
     (dict(), "packed", dict(rows_per_wave=1, ycoop=7, ycoop_order=4, ylds=0, handoff_batch=4)),
-    # c3 (half-widths 4-64): table 4 rows per wave, no LDS staging, one hand-off per call; packed 2 rows
+    # c3 (half-widths 4-64): table 4 rows per wave (ypass_table_kernel), no LDS staging, two generations per
+    # hand-off, the run generation; packed 2 rows, one hand-off per call
     (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "table",
-     dict(rows_per_wave=4, ylds=0, handoff_batch=1, ycoop=0, gen_dense=1)),
+     dict(rows_per_wave=4, ylds=0, handoff_batch=2, ycoop=0, gen_dense=2, ydepth=1)),
     (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "packed",
      dict(rows_per_wave=2, ylds=0, ycoop=0, handoff_batch=1)),
     # c2: epochs of 2

@@ -33,7 +33,7 @@ CFG = {"c1": (128, 128, 8, 8), "c2": (512, 512, 4, 32), "c3": (2048, 2048, 4, 64
 
 def make(envspec, cfg, mode, rpw):
     saved = {}
-    for kv in filter(None, envspec.split(",")):
+    for kv in filter(None, envspec.replace(":", ",").split(",")):
         k, v = kv.split("=")
         saved[k] = os.environ.get(k)
         os.environ[k] = v
@@ -63,12 +63,13 @@ def main():
     ap.add_argument("--tune-b", default=None)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=10)
+    ap.add_argument("--events", type=int, default=1, help="0: wall time only (no per-call phase events)")
     a = ap.parse_args()
     tune = None
     if a.tune_a is not None or a.tune_b is not None:
         one = make(a.a, a.config, a.mode, a.rpw_a)
         hs = {"A": one, "B": one}
-        tune = {k: [(kv.split("=")[0], int(kv.split("=")[1])) for kv in filter(None, (v or "").split(","))]
+        tune = {k: [(kv.split("=")[0], int(kv.split("=")[1])) for kv in filter(None, (v or "").replace(":", ",").split(","))]
                 for k, v in (("A", a.tune_a), ("B", a.tune_b))}
     else:
         hs = {"A": make(a.a, a.config, a.mode, a.rpw_a), "B": make(a.b, a.config, a.mode, a.rpw_b)}
@@ -83,14 +84,14 @@ def main():
                 for key, val in tune[k]:
                     f.set_tuning(key, val)
                 f.filter(1e-8)  # first call after a switch is not timed
-            f.set_profiling(True)
+            f.set_profiling(bool(a.events))
             f.sync()
             t0 = time.perf_counter()
             for _ in range(a.calls):
                 f.filter(1e-8)
             f.sync()
             wall = (time.perf_counter() - t0) * 1e3 / a.calls
-            p = f.profile()
+            p = f.profile() if a.events else {"calls": 1, "rng_ms": 0, "ypass_ms": 0, "zpass_ms": 0, "total_ms": 0}
             f.set_profiling(False)
             p["wall_ms"] = wall * p["calls"]
             for ph in rec[k]:

@@ -28,7 +28,10 @@ p.add_argument("--replicate", type=int, default=1)
 p.add_argument("--ns", default="1,2,4,8")
 p.add_argument("--calls", type=int, default=20)
 p.add_argument("--tune", default="", help="k=v:k=v... df_set_tuning before the warm-up")
+p.add_argument("--env", default="", help="K=V:K=V... environment knobs set before the library loads")
 a = p.parse_args()
+for kv in filter(None, a.env.split(":")):
+    os.environ[kv.split("=")[0]] = kv.split("=")[1]
 os.environ["DFAMD_RNG_REPLICATE"] = str(a.replicate)
 import dfamd  # noqa: E402
 

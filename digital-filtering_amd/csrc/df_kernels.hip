@@ -1014,9 +1014,18 @@ __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &
     return true;
 }
 
-// K3r: one wave per piece (see above). The ring holds the state one step into each attempt (s1: the screen
-// walks s1 and s3 with one multiply-add each per group); s0 = one step back when the chunk is generated.
-__global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+#if defined(DF_K3R_WPE)
+#define DF_K3R_ATTR __attribute__((amdgpu_waves_per_eu(DF_K3R_WPE)))
+#else
+#define DF_K3R_ATTR
+#endif
+// K3r: one wave per piece (see above). RECOUNT (split counting): each lane screens its attempt of the group as
+// K1 does; the walk keeps the states one and three steps into the attempt (s1, s3: one multiply-add each per
+// group), the ring holds s1, and s0 = one step back when the chunk is generated. Otherwise (one GPU) the flags
+// are K1's masks: the 16 groups of one (block, wave) share a 16-bit word per lane (word (G >> 4) * 64 + lane,
+// bit G & 15), loaded once and the next one ahead; the walk keeps s0 alone.
+template <bool RECOUNT>
+__global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                       RngStateDev *__restrict__ sout,
                                                                       const uint16_t *__restrict__ masks,
                                                                       int *__restrict__ err)
@@ -1045,42 +1054,57 @@ __global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g
     G = uniform((int)G);
     long long R = c0 * 64 - uniform(skip); // rank of group G's first accepted attempt
     const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
-    // lane's attempt 64 G + lane: its start state s0, then s1 (1 step) and s3 (3 steps) for the screen
-    uint64_t s1, s3;
+    // lane's attempt 64 G + lane: its start state s0 (RECOUNT: s1, 1 step on, and s3, 3 steps on, instead)
+    uint64_t st, s3 = 0;
     {
         const uint64_t S = sin->state;
         const PcgJumpDev jb = g.jump_block[G >> 6], jg = g.jump_gi[G & 63], jl = g.jump_lane[lane];
-        const uint64_t s0 = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
-        s1 = s0 * kPcgMult + kPcgInc;
-        s3 = s1 * kPcgMult2 + kPcgInc2;
+        st = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
+        if (RECOUNT) {
+            st = st * kPcgMult + kPcgInc;
+            s3 = st * kPcgMult2 + kPcgInc2;
+        }
+    }
+    const long long nwords = g.nb_groups >> 4; // mask words per lane in the call
+    uint32_t mw = 0, mw_next = 0;
+    if (!RECOUNT) {
+        mw = masks[(size_t)(G >> 4) * 64 + lane];
+        mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
     }
     long long c = c0;
     int top = 0;
     while (c < cend && G < g.nb_groups) { // uniform; the group bound only matters after a shortage (err set)
         bool acc;
-        if (g.recount) {
-            const int v = polar_screen13(s1, s3);
+        if (RECOUNT) {
+            const int v = polar_screen13(st, s3);
             acc = v > 0;
             if (v < 0) { // ~2e-5 of the attempts: the exact double test (random.tcc:1822-1826), as K1
-                uint64_t s0 = (s1 - kPcgInc) * kPcgMultInv;
+                uint64_t s0 = (st - kPcgInc) * kPcgMultInv;
                 acc = polar_attempt(s0).accept;
             }
         } else {
-            const long long b = G >> 6;
-            const int gi = (int)(G & 63);
-            acc = (masks[(size_t)b * kRngThreads + (gi >> 4) * 64 + lane] >> (gi & 15)) & 1u;
+            acc = (mw >> (G & 15)) & 1u;
         }
         const uint64_t m = __ballot(acc);
         const long long rank = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = s1;
+        if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = st;
         R += __popcll(m);
         ++G;
-        s1 = g.next_mult * s1 + g.next_plus1;
-        s3 = g.next_mult * s3 + g.next_plus3;
+        if (RECOUNT) {
+            st = g.next_mult * st + g.next_plus1;
+            s3 = g.next_mult * s3 + g.next_plus3;
+        } else {
+            st = g.next_mult * st + g.next_plus;
+            if ((G & 15) == 0) { // the next (block, wave) word; the one after it in flight
+                mw = mw_next;
+                mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
+            }
+        }
         __asm__ volatile("" ::: "memory"); // wave-private ring: only the compiler must keep the order
         while (c < cend && R >= min((c + 1) * 64, A)) { // every rank of chunk c is in the ring
-            const uint64_t s = (ring[(c * 64 + lane) & 127] - kPcgInc) * kPcgMultInv;
+            const uint64_t rs = ring[(c * 64 + lane) & 127];
+            const uint64_t s = RECOUNT ? (rs - kPcgInc) * kPcgMultInv : rs;
             dense_chunk(g, f, A, c, (int)pc.li0 + (int)(c - c0), s, lane, defer, stk, top, sout);
             ++c;
         }
@@ -1204,8 +1228,12 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
 #endif
     if (g.gen_dense == 2) { // run generation: K3r alone (K2s ran with K1, before any exchange)
         const int np = g.npieces[0] > g.npieces[1] ? g.npieces[0] : g.npieces[1];
-        hipLaunchKernelGGL(rng_run_generate_kernel, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in, st_out,
-                           masks, err);
+        if (g.recount)
+            hipLaunchKernelGGL(rng_run_generate_kernel<true>, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in,
+                               st_out, masks, err);
+        else
+            hipLaunchKernelGGL(rng_run_generate_kernel<false>, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in,
+                               st_out, masks, err);
         return hipGetLastError();
     }
     if (g.gen_dense) {

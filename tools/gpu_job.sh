@@ -12,6 +12,7 @@
 #   prof[=BENCH_ARGS]         rocprofv3 --kernel-trace --stats -- python3 bench.py ...     600 s
 #   py=SCRIPT[,ARGS]          python3 SCRIPT ARGS (commas become spaces)                   400 s
 #   rocpy=SCRIPT[,ARGS]       rocprofv3 --kernel-trace --stats -- python3 SCRIPT ARGS       400 s
+#   sh=SCRIPT[,ARGS]          bash SCRIPT ARGS (a tools/ script)                           400 s
 #   smoke                     __graft_entry__.smoke()                                      300 s
 # Outputs: gpurun_out/TAG/<i>_<step>.{log,json}.
 set -o pipefail
@@ -49,6 +50,8 @@ for step in "$@"; do
         (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$base.d" -o run -- \
             python3 "$ROOT/$script" "$@" > "$base.log" 2>&1); rc=$?
         [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && head -25 "$base.split.csv" ;;
+    sh) set -- $arg; script=$1; shift
+        timeout -k 10 400 bash "$script" "$@" > "$base.log" 2>&1; rc=$?; tail -30 "$base.log" ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$base.log" 2>&1; rc=$?; tail -2 "$base.log" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac

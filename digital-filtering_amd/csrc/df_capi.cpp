@@ -1519,7 +1519,8 @@ int alloc_dense(df_handle *h)
     h->geom.cstate = cs;
     // Run generation (gen_dense 2): the list cut into pieces of consecutive chunks, at most kRunPiece each and
     // of near-equal length within a run (a 9-chunk row segment of a strip is one piece, not 8 + 1)
-    constexpr uint32_t kRunPiece = 12;
+    uint32_t kRunPiece = 12;
+    if (const char *e = std::getenv("DFAMD_RUN_PIECE")) kRunPiece = (uint32_t)std::max(1, std::atoi(e));
     for (int f = 0; f < 2; ++f) {
         std::vector<RunPiece> pcs;
         const std::vector<uint32_t> &L = list[f];

@@ -162,6 +162,10 @@ struct df_handle {
     // RCCL operation per df_filter (north star) - and the rest of that generation runs after the group, beside
     // the z-pass. gen_pending: K1 enqueued, the exchange and gen_end not yet.
     int fused_x = 1;
+    // Generations enqueued ahead of the step that consumes them (fused exchange): 2 = the share records of
+    // generation k + 2 travel in call k's halo group and its K3r runs during call k + 1, so the RNG chain has a
+    // whole call to finish instead of the z-pass beside it (4 noise sets). 1 = generation k + 1 in call k.
+    int look = 1;
     bool gen_pending = false;
     RngGeom pend_g{};
     hipEvent_t ev_xchg = nullptr; // DFAMD_SOLO_STRIP: where the halo group would sit (after the pack)
@@ -616,13 +620,14 @@ int consume_gen(df_handle *h)
 // so the last generation of epoch e + 1 goes
 // under the last step of epoch e, just before epoch e + 1 waits for it.
 int fused_gen_end(df_handle *h);
+bool fused_active(const df_handle *h);
 int prefetch_gen(df_handle *h)
 {
     if (int rc = fused_gen_end(h)) return rc;
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
     (void)gi;
-    const long long need = h->gen_used + h->hb;
+    const long long need = h->gen_used + (fused_active(h) ? h->look : h->hb);
     int rc;
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
@@ -641,7 +646,7 @@ bool fused_active(const df_handle *h)
 int fused_gen_begin(df_handle *h)
 {
     h->gen_pending = false; // a K1 left pending by a failed call is simply redone
-    if (!fused_active(h) || h->gen_launched != h->gen_used) return DF_OK;
+    if (!fused_active(h) || h->gen_launched != h->gen_used + (h->look - 1)) return DF_OK;
     hipStream_t rs;
     int rc = gen_begin(h, h->pend_g, rs);
     if (rc) return rc;
@@ -1606,6 +1611,10 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
     h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
+    // z-strip handles in table mode (split counting, the fused exchange): generations two calls ahead
+    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE) h->look = 2;
+    if (const char *e = std::getenv("DFAMD_LOOKAHEAD")) h->look = std::atoi(e) >= 2 ? 2 : 1;
+    if (h->look == 2) h->nsets = 4;
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;

@@ -41,13 +41,13 @@ for step in "$@"; do
            echo "wall_s $(( $(date +%s) - start ))" | tee "$base.wall"
            [ $rc -eq 0 ] && python3 tools/bench_summary.py "$base.json" ;;
     strip) timeout -k 10 400 python3 tools/strip_timing.py $arg > "$base.json" 2> "$base.log"; rc=$?; cat "$base.json" ;;
-    prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$base.d" -o run -- \
+    prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$base.d" -o run -- \
              python3 "$ROOT/bench.py" $arg > "$base.log" 2>&1); rc=$?
           [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && head -25 "$base.split.csv" ;;
     py) set -- $arg; script=$1; shift
         timeout -k 10 400 python3 "$script" "$@" > "$base.log" 2>&1; rc=$?; tail -30 "$base.log" ;;
     rocpy) set -- $arg; script=$1; shift
-        (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$base.d" -o run -- \
+        (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$base.d" -o run -- \
             python3 "$ROOT/$script" "$@" > "$base.log" 2>&1); rc=$?
         [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && head -25 "$base.split.csv" ;;
     sh) set -- $arg; script=$1; shift

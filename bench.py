@@ -40,6 +40,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "digital-filtering_amd")
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FIELDS = ("u", "v", "w", "T", "rho")
+RNG_COLLECTIVE = {  # df_comm_stats.rng_collective (include/df_c.h)
+    0: "none: every rank counts the whole stream (replicated), halo is the only collective",
+    1: "allgather: share records (per-64-attempt accept counts) on a second communicator",
+    2: "in the halo group: share records of a later generation ride in the call's ncclGroup (one grouped op per call)",
+}
 
 # name: plane, Ny, Nz (whole plane), N_min, N_max, description
 CONFIGS = {
@@ -137,7 +142,7 @@ def launch_command(argv, n, port):
 
 
 PROGRESS_ENV = "DFAMD_PROGRESS_DIR"
-LAUNCH_TIMEOUT_S = 1500  # the whole N-rank job; a bare 8-GPU run takes a few minutes (profiles/r4/bench8_emulated)
+LAUNCH_TIMEOUT_S = 1500  # the whole N-rank job; a bare 8-GPU run takes a few minutes (profiles/r4/j: 515 s with emulated hosts)
 
 
 def rank_phase(name, rank=None):
@@ -647,8 +652,7 @@ def summarize(ctx, wl, args, recs):
         cm = recs[0]["comm"] or {}
         out["multi_gpu"] = {
             "rccl_ranks": cm.get("rccl_ranks"),
-            "rng_collective": ("allgather(block and wave accept counts; K3 recounts its waves' flags)" if cm.get("rng_collective")
-                               else "none: every rank counts the whole stream (replicated), halo is the only collective"),
+            "rng_collective": RNG_COLLECTIVE.get(cm.get("rng_collective", 0), "?"),
             "halo_ms_per_call": {"max": max(r["phase_ms_per_call"]["halo_ms"] for r in recs),
                                  "min": min(r["phase_ms_per_call"]["halo_ms"] for r in recs)},
             "halo_bytes_per_call": sum((r["comm"] or {}).get("halo_bytes_sent", 0) for r in recs),
@@ -857,7 +861,7 @@ def main(argv=None):
                        "parallelism": f"z-strips x{ctx.world}" if ctx.world > 1 else "single GPU"},
             "emulated_hosts": ctx.emulated or None,
             "parity_ok": parity["ok"] if parity else None,
-            "rng_collective": "allgather" if (comm or {}).get("rng_collective") else "none",
+            "rng_collective": RNG_COLLECTIVE.get((comm or {}).get("rng_collective", 0), "?").split(":")[0],
             "phase_ms_per_call": head["phase_ms_per_call"],
             "roofline": head["roofline"],
             "cpu_baseline": cpu,

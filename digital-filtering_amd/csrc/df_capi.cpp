@@ -2399,7 +2399,8 @@ int df_comm_info(df_handle *h, df_comm_stats *out)
     const bool split = h->world > 1 || h->halo_loopback;
     out->halo_peers = h->world > 1 ? (h->rank > 0) + (h->rank < h->world - 1) : (h->halo_loopback ? 2 : 0);
     out->halo_bytes_sent = split ? (long long)out->halo_peers * (long long)h->halo_elems * 8 : 0;
-    out->rng_collective = h->split_count && h->rng_comm ? 1 : 0;
+    // 2: the records ride in the halo's ncclGroup (one grouped RCCL operation per call); 1: an all-gather of their own
+    out->rng_collective = h->split_count && h->rng_comm ? (fused_active(h) ? 2 : 1) : 0;
     const long long others = (long long)h->rng_chunk * (h->world - 1);
     long long rec = 0, lo = 0, to = 0;
     record_layout(h->rng_chunk, &rec, &lo, &to);

@@ -252,15 +252,18 @@ int df_comm_unique_id(void *out, size_t len); /* RCCL unique id, len >= 128 */
  * rccl_ranks comes from ncclCommCount on the handle's communicator (0: no RCCL). The collective
  * form follows coeff_mode: DF_COEFF_PACKED replicates the counting, so the halo send/recv is the
  * call's only collective (rng_collective 0); DF_COEFF_TABLE (the df_config_default mode) splits the
- * counting and adds one all-gather of block and wave accept counts per call (rng_collective 1) - only
- * counts travel, K3 recomputes the accept flags of the waves it runs. df_set_tuning(h,
- * "rng_replicate", 0 | 1) overrides either default (alike on every rank, before the first df_filter). */
+ * counting: each rank counts 1/N of the attempt blocks and the ranks exchange share records (per
+ * 64-attempt accept counts, the share's block prefix and its total). With the run generation and
+ * "fused_exchange" (the defaults) the records of a later generation travel inside the call's halo
+ * ncclGroup, so a call issues ONE grouped RCCL operation (rng_collective 2); otherwise they are
+ * all-gathered on a second communicator (rng_collective 1). df_set_tuning(h, "rng_replicate", 0 | 1)
+ * overrides the counting form (alike on every rank, before the first df_filter). */
 typedef struct df_comm_stats {
     int rccl_ranks, rccl_rank;    /* ncclCommCount / ncclCommUserRank; 0, 0 without RCCL */
     int halo_peers;               /* neighbours this strip exchanges z-halo columns with (0-2) */
-    int rng_collective;           /* 1: per-call RNG all-gather (split counting); 0: none */
+    int rng_collective;           /* 2: records in the halo group; 1: an RNG all-gather; 0: none */
     long long halo_bytes_sent;    /* per df_filter, all three components */
-    long long rng_bytes_received; /* per df_filter, RNG all-gather (0 when replicated) */
+    long long rng_bytes_received; /* per df_filter, RNG share records (0 when replicated) */
     long long rng_blocks_counted; /* attempt blocks of 4096 this rank tests per call (K1) */
     long long rng_blocks_total;   /* attempt blocks of the whole plane's call */
 } df_comm_stats;

@@ -138,6 +138,7 @@ struct df_handle {
     int halo_loopback = 0; // one-rank communicator: send the halo columns to itself and check them (2: corrupt one)
     int overlap = 1; // generate the next call's noise on rng_stream during this call's sweeps
     int solo_strip = 0; // timing only: one strip of a split plane, halo never exchanged (DFAMD_SOLO_STRIP)
+    double solo_xchg_us = 0; // timing only: a solo strip's exchange held for this long (DFAMD_SOLO_XCHG_US)
     CompDev c[3];
     double *T = nullptr, *rho = nullptr, *rowc = nullptr, *tab = nullptr, *tabf = nullptr;
     int *tab_off = nullptr, *tabf_off = nullptr;
@@ -744,8 +745,9 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
 int phase_halo_rccl(df_handle *h)
 {
     if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
-    if (h->solo_strip) { // timing only: the pack, no exchange
+    if (h->solo_strip) { // timing only: the pack, no exchange (or a hold of DFAMD_SOLO_XCHG_US in its place)
         int rc = phase_halo_pack(h);
+        if (!rc && h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, h->stream), DF_EHIP);
         if (!rc && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->stream), DF_EHIP);
         return rc;
     }
@@ -789,9 +791,10 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     }
     if ((rc = phase_halo_pack(h))) return rc;
     HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
-    if (!peer && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->stream), DF_EHIP);
     ev_record(h, 2); // halo_ms is the pack alone here; the exchange runs under zpass_ms
     HIP_OR(hipStreamWaitEvent(h->comm_stream, h->ev_packed, 0), DF_EHIP);
+    if (!peer && h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, h->comm_stream), DF_EHIP);
+    if (!peer && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->comm_stream), DF_EHIP);
     // From here on comm_stream holds work that reads the send buffers: whatever fails below, the stream
     // joins comm_stream before returning, so the next call's pack cannot overwrite buffers still in flight.
     auto join = [h](int code) {
@@ -904,6 +907,7 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_ZUNROLL")) h->zunroll = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
+    if (const char *e = std::getenv("DFAMD_SOLO_XCHG_US")) h->solo_xchg_us = h->solo_strip ? std::atof(e) : 0;
     // Table mode splits the counting (one small all-gather of counts beside the halo): its sweeps are
     // VALU-bound like the RNG, so every rank counting the whole stream shows (one rank of a c4 split
     // in 8: 0.28-0.30 -> 0.24-0.27 ms per call). Packed keeps the halo as the call's only collective:

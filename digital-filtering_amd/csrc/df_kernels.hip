@@ -2698,6 +2698,23 @@ __global__ void halo_check_kernel(const double *__restrict__ sent, const double 
     }
 }
 
+// Timing only (DFAMD_SOLO_XCHG_US): one wave that holds its stream for `ticks` of the 100 MHz real-time
+// clock, standing in for the exchange of a solo-strip handle. Bounded: at most 2^20 sleeps (~60 ms).
+__global__ void hold_kernel(unsigned long long ticks)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+hipError_t launch_hold(double us, hipStream_t st)
+{
+    hold_kernel<<<1, 64, 0, st>>>((unsigned long long)(us * 100.0));
+    return hipGetLastError();
+}
+
 hipError_t launch_halo_check(const double *sent, const double *got, size_t n, int corrupt, int *bad, hipStream_t st)
 {
     hipLaunchKernelGGL(halo_check_kernel, dim3(256), dim3(256), 0, st, sent, got, n, corrupt, bad);

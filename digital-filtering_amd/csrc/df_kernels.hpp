@@ -193,6 +193,7 @@ hipError_t launch_gather(const double *src, long long nsrc, long long n, const l
                          const long long *didx, long long ndst, double beta, int *bad, hipStream_t st);
 hipError_t launch_halo_pack(const SweepArgs &a, double *send_l, double *send_r, hipStream_t st);
 hipError_t launch_halo_unpack(const SweepArgs &a, const double *recv_l, const double *recv_r, hipStream_t st);
+hipError_t launch_hold(double us, hipStream_t st); // timing only: a stand-in exchange of us microseconds
 hipError_t launch_halo_check(const double *sent, const double *got, size_t n, int corrupt, int *bad, hipStream_t st);
 
 } // namespace dfamd

@@ -181,6 +181,13 @@ struct df_handle {
     // edge launch runs unstaged, against an exchange of a few tens of us).
     int halo_overlap = -1;
     hipStream_t comm_stream = nullptr;
+    // Table z-strips with the fused exchange (round 4): K3r on a stream of its own, behind K3e, which writes the
+    // generation's end state right after the exchange - so the next generation's count never waits for this
+    // one's generation (the state chain is K1 -> exchange -> K3e only). Records double-buffered by generation.
+    hipStream_t gen_stream = nullptr;
+    hipEvent_t ev_state = nullptr, ev_k3r_done[2] = {nullptr, nullptr};
+    size_t xhalf = 0; // bytes of one record buffer when double-buffered (0: one buffer)
+    int decouple = 1; // DFAMD_GEN_DECOUPLE (timing A/B): 0 keeps K3r on rng_stream, writing the end state itself
     hipEvent_t ev_packed = nullptr, ev_unpacked = nullptr; // halo packed (stream); edge strips done (comm_stream)
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
     long long gen_launched = 0; // generations enqueued (generation n reads state slot n%nsets, writes (n+1)%nsets)
@@ -397,10 +404,10 @@ int check_rng_error(df_handle *h)
 
 bool prof_on(df_handle *h) { return h->profiling && h->prof_call && h->ev_used < h->ev.size(); }
 
-void ev_record(df_handle *h, int phase)
+void ev_record(df_handle *h, int phase, hipStream_t st = nullptr)
 {
     if (!prof_on(h)) return;
-    (void)hipEventRecord(h->ev[h->ev_used].e[phase], phase >= 4 && h->overlap ? h->rng_stream : h->stream);
+    (void)hipEventRecord(h->ev[h->ev_used].e[phase], st ? st : phase >= 4 && h->overlap ? h->rng_stream : h->stream);
 }
 
 int sync_all(df_handle *h)
@@ -408,6 +415,7 @@ int sync_all(df_handle *h)
     HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     if (h->comm_stream) HIP_OR(hipStreamSynchronize(h->comm_stream), DF_EHIP);
+    if (h->gen_stream) HIP_OR(hipStreamSynchronize(h->gen_stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -466,12 +474,15 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
         HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e & 1], 0), DF_EHIP);
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
+    g.end_ext = 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
     g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? h->gen_dense : 0;
     if (g.gen_dense == 2) { // K1 writes the group counts of its share's record, K2s the share's prefix
-        g.xbuf = h->xbuf;
+        g.xbuf = h->xbuf + (h->xhalf ? (size_t)(gi & 1) * h->xhalf : 0);
+        // double-buffered records: the K3r of generation gi - 2 (gen_stream) read this buffer last
+        if (h->xhalf && h->gen_stream) HIP_OR(hipStreamWaitEvent(rs, h->ev_k3r_done[gi & 1], 0), DF_EHIP);
         g.xworld = h->split_count ? h->world : 1;
         g.xchunk = h->split_count ? h->rng_chunk : h->rng_blocks;
         record_layout(g.xchunk, &g.xstride, &g.xlp_off, &g.xtot_off);
@@ -511,9 +522,10 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
                              h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks, h->err_dev,
                              h->rng_blocks, nb_scan, rs),
            DF_EHIP);
-    if (prof_on(h)) ev_record(h, 5);
+    if (prof_on(h)) ev_record(h, 5, rs);
     if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
+    if (h->xhalf && h->gen_stream && g.gen_dense == 2) HIP_OR(hipEventRecord(h->ev_k3r_done[gi & 1], rs), DF_EHIP);
     h->gen_launched++;
     return DF_OK;
 }
@@ -545,7 +557,7 @@ int launch_gen_group(std::vector<df_handle *> &hs)
                                   (size_t)h->rng_chunk * kWavesPerBlock * sizeof(int), hipMemcpyDefault, rss[r]),
                    DF_EHIP);
             if (gs[r].gen_dense == 2)
-                HIP_OR(hipMemcpyAsync(h->xbuf + (size_t)o * gs[r].xstride, hs[o]->xbuf + (size_t)o * gs[r].xstride,
+                HIP_OR(hipMemcpyAsync(gs[r].xbuf + (size_t)o * gs[r].xstride, gs[o].xbuf + (size_t)o * gs[r].xstride,
                                       (size_t)gs[r].xstride, hipMemcpyDefault, rss[r]),
                        DF_EHIP);
         }
@@ -570,7 +582,7 @@ int launch_gen(df_handle *h)
         const size_t nwc = (size_t)h->rng_chunk * kWavesPerBlock;
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
         const size_t ngc = (size_t)g.xstride;
-        uint8_t *gmine = h->xbuf + (size_t)h->rank * ngc;
+        uint8_t *gmine = g.xbuf + (size_t)h->rank * ngc;
         if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
             // Never concurrent with the halo send/recv of the other communicator: every rank issues
             // the all-gather only after its own halo group of the call just enqueued has completed,
@@ -578,14 +590,14 @@ int launch_gen(df_handle *h)
             if (h->ev_halo) HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
             NCCL_OR(ncclGroupStart());
             if (g.gen_dense == 2) { // run form: the group counts alone (block counts are their sums)
-                NCCL_OR(ncclAllGather(gmine, h->xbuf, ngc, ncclUint8, h->rng_comm, rs));
+                NCCL_OR(ncclAllGather(gmine, g.xbuf, ngc, ncclUint8, h->rng_comm, rs));
             } else {
                 NCCL_OR(ncclAllGather(mine, h->counts, h->rng_chunk, ncclInt, h->rng_comm, rs));
                 NCCL_OR(ncclAllGather(wmine, h->wave_counts, nwc, ncclInt, h->rng_comm, rs));
             }
             NCCL_OR(ncclGroupEnd());
         } else if (g.gen_dense == 2) { // DFAMD_SOLO_STRIP: this rank's group counts stand in for every share
-            HIP_OR(launch_replicate_share(h->xbuf, ngc, h->world, h->rank, rs), DF_EHIP);
+            HIP_OR(launch_replicate_share(g.xbuf, ngc, h->world, h->rank, rs), DF_EHIP);
         } else { // DFAMD_SOLO_STRIP timing mode: stand-in shares for the other ranks
             for (int o = 0; o < h->world; ++o)
                 if (o != h->rank) {
@@ -670,9 +682,17 @@ int fused_gen_end(df_handle *h)
         HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
     } else { // solo strip: the same dependency on this call's halo position, the exchange by a stand-in copy
         HIP_OR(hipStreamWaitEvent(rs, h->ev_xchg, 0), DF_EHIP);
-        HIP_OR(launch_replicate_share(h->xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
+        HIP_OR(launch_replicate_share(h->pend_g.xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
     }
-    return gen_end(h, h->pend_g, rs);
+    if (!h->gen_stream || !h->decouple) return gen_end(h, h->pend_g, rs);
+    // K3e: the end state (next generation's start) right after the exchange, on rng_stream; K3r on gen_stream
+    const long long gi = h->gen_launched;
+    HIP_OR(launch_rng_end_state(h->pend_g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->err_dev, rs),
+           DF_EHIP);
+    HIP_OR(hipEventRecord(h->ev_state, rs), DF_EHIP);
+    HIP_OR(hipStreamWaitEvent(h->gen_stream, h->ev_state, 0), DF_EHIP);
+    h->pend_g.end_ext = 1;
+    return gen_end(h, h->pend_g, h->gen_stream);
 }
 
 int phase_ypass(df_handle *h, int comps_mask)
@@ -730,7 +750,7 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
     NCCL_OR(ncclGroupStart());
     if (h->gen_pending) { // fused exchange: the next generation's share records, in place, in the same group
         const size_t ngc = (size_t)h->pend_g.xstride;
-        NCCL_OR(ncclAllGather(h->xbuf + (size_t)h->rank * ngc, h->xbuf, ngc, ncclUint8, h->comm, st));
+        NCCL_OR(ncclAllGather(h->pend_g.xbuf + (size_t)h->rank * ngc, h->pend_g.xbuf, ngc, ncclUint8, h->comm, st));
     }
     if (h->rank > 0) {
         NCCL_OR(ncclSend(h->send_l, h->halo_elems, ncclDouble, h->rank - 1, h->comm, st));
@@ -1443,7 +1463,10 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         long long st1 = 0, stw = 0, lo, to;
         record_layout(h->rng_blocks, &st1, &lo, &to);
         record_layout(h->rng_chunk, &stw, &lo, &to);
-        if ((rc = dalloc_t(h, &h->xbuf, (size_t)std::max(st1, stw * h->world)))) return rc;
+        const size_t xb = (size_t)std::max(st1, stw * h->world);
+        // table z-strips: two record buffers (generation parity), so K3r may run behind the next generation's K1
+        h->xhalf = h->world > 1 && h->coeff_mode == DF_COEFF_TABLE ? (xb + 255) / 256 * 256 : 0;
+        if ((rc = dalloc_t(h, &h->xbuf, h->xhalf ? 2 * h->xhalf : xb))) return rc;
         if (h->world > 64) return fail(DF_EINVAL, "more than 64 z-strip ranks"); // run generation's share lookup
     }
     h->geom.nb_groups = (long long)h->rng_blocks * 64;
@@ -1545,33 +1568,78 @@ int alloc_dense(df_handle *h)
         for (uint64_t c = 0; c < nch; ++c)
             if ((bits[f][c >> 5] >> (c & 31)) & 1u) list[f].push_back((uint32_t)c);
     }
-    // K3a / K3r fast chunks: all 128 positions in one r_ys array (one GPU: every column stored, at most one row
-    // wrap; a z-strip: inside the strip's columns of one row), every rank live and none the call's last (that one
-    // sets the stream state): destinations by arithmetic
+    // K3a / K3r fast chunks: no rank past the call or the call's last (that one sets the stream state), all 128
+    // positions in one stream array with at most one row wrap, and the positions this GPU stores (stream_dest:
+    // r_ys columns [z0, z1), the r_zs pads of the plane's edge strips) one run [lo, hi) whose destinations are
+    // affine in the position on either side of the wrap: destinations by arithmetic. Round 4: r_zs pads and
+    // partial chunks (a strip's first and last of each row) too, not only whole r_ys chunks.
+    auto dest_of = [&g](int su, uint64_t row, uint64_t col, long long &off) { // host mirror of stream_dest
+        const int cmp = su >> 1;
+        if ((su & 1) == 0) {
+            if (col < (uint64_t)g.z0 || col >= (uint64_t)g.z1) return false;
+            off = (long long)(row * (uint64_t)g.Pz + (col - (uint64_t)g.z0));
+            return true;
+        }
+        long long lc;
+        if (col < (uint64_t)g.Nzp[cmp]) {
+            if (!g.is_first) return false;
+            lc = (long long)col;
+        } else if (col >= (uint64_t)(g.Nzp[cmp] + g.Nz_g)) {
+            if (!g.is_last) return false;
+            lc = (long long)col - g.z0;
+        } else {
+            return false;
+        }
+        off = (long long)(row * (uint64_t)g.rz_pitch[cmp]) + lc;
+        return true;
+    };
     std::vector<ChunkDest> dest[2];
     for (int f = 0; f < 2; ++f) {
         const long long A = (long long)((g.Q - f + 1) / 2);
-        dest[f].resize(std::max<size_t>(1, list[f].size()), ChunkDest{0, 0, 0, -1, 0});
+        dest[f].resize(std::max<size_t>(1, list[f].size()), ChunkDest{0, 0, 0, -1, 0, 0});
         for (size_t i = 0; i < list[f].size(); ++i) {
             const uint64_t c = list[f][i], q0 = f + 128 * c;
             if ((long long)(64 * c + 63) >= A - 1) continue;
             int su = 0;
             while (su < 5 && q0 >= g.seg[su + 1]) ++su;
             const uint64_t W = g.width[su];
-            if ((su & 1) || W < 128 || q0 + 128 > g.seg[su + 1]) continue;
-            const uint64_t p = q0 - g.seg[su], row = p / W, col = p % W;
-            ChunkDest d{};
-            if (g.z0 == 0 && (uint64_t)g.z1 == W) { // every column stored: at most one row wrap
-                d.off = (long long)(row * (uint64_t)g.Pz + col);
-                d.wr = (short)std::min<uint64_t>(128, W - col);
-                d.jump = g.Pz - (int)W;
-            } else { // a z-strip: the chunk's 128 positions inside this strip's columns of one row (round 4)
-                if (col < (uint64_t)g.z0 || col + 128 > (uint64_t)g.z1) continue;
-                d.off = (long long)(row * (uint64_t)g.Pz + (col - (uint64_t)g.z0));
-                d.wr = 128;
-                d.jump = 0;
+            if (q0 + 128 > g.seg[su + 1] || W == 0) continue;
+            uint64_t row = (q0 - g.seg[su]) / W, col = (q0 - g.seg[su]) % W;
+            int lo = -1, hi = -1, wr = 128, wraps = 0;
+            long long d0 = 0, d1 = 0;
+            bool ok = true;
+            for (int e = 0; e < 128 && ok; ++e) {
+                long long off;
+                if (dest_of(su, row, col, off)) {
+                    const long long d = off - e;
+                    if (lo < 0) {
+                        lo = e;
+                        d0 = d1 = d;
+                    } else if (hi >= 0) {
+                        ok = false; // a second run
+                    } else if (d != d1) {
+                        if (d1 != d0) ok = false; // a second change of the affine map
+                        d1 = d;
+                        wr = e;
+                    }
+                } else if (lo >= 0 && hi < 0) {
+                    hi = e;
+                }
+                if (++col == W) {
+                    col = 0;
+                    ++row;
+                    ++wraps;
+                }
             }
+            if (!ok || lo < 0 || wraps > 1) continue;
+            if (hi < 0) hi = 128;
+            ChunkDest d{};
+            d.off = d0;
+            d.jump = (int)(d1 - d0);
+            d.wr = (uint8_t)wr;
             d.arr = (signed char)su;
+            d.lo = (uint8_t)lo;
+            d.hi = (uint8_t)hi;
             dest[f][i] = d;
         }
     }
@@ -1641,6 +1709,12 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         int prio_lo = 0, prio_hi = 0;
         HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
         HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
+        if (h->xhalf && h->overlap) {
+            HIP_OR(hipStreamCreateWithFlags(&h->gen_stream, hipStreamNonBlocking), DF_EHIP);
+            HIP_OR(hipEventCreateWithFlags(&h->ev_state, hipEventDisableTiming), DF_EHIP);
+            for (auto &e : h->ev_k3r_done) HIP_OR(hipEventCreateWithFlags(&e, hipEventDisableTiming), DF_EHIP);
+            if (const char *e = std::getenv("DFAMD_GEN_DECOUPLE")) h->decouple = std::atoi(e);
+        }
         HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_xchg, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
@@ -1721,6 +1795,7 @@ void destroy(df_handle *h)
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
+    if (h->gen_stream) (void)hipStreamSynchronize(h->gen_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
     for (void *p : h->allocs) {
@@ -1738,6 +1813,10 @@ void destroy(df_handle *h)
     }
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
+    if (h->gen_stream) (void)hipStreamDestroy(h->gen_stream);
+    if (h->ev_state) (void)hipEventDestroy(h->ev_state);
+    for (auto &e : h->ev_k3r_done)
+        if (e) (void)hipEventDestroy(e);
     if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
     if (h->ev_xchg) (void)hipEventDestroy(h->ev_xchg);
     if (h->ev_unpacked) (void)hipEventDestroy(h->ev_unpacked);

@@ -49,14 +49,15 @@ struct WaveTask {
     int gw, pad;
 };
 
-// K3a destination of a 128-position chunk (host-built, RngGeom::chunk_dest): position i of the chunk goes to
-// r_ys[arr >> 1] + off + i, plus jump once i >= wr (the row wrap: pitch - width).
+// K3a / K3r destination of a 128-position chunk (host-built, RngGeom::chunk_dest): position i of the chunk, if
+// lo <= i < hi, goes to buffer arr + off + i, plus jump once i >= wr (one row wrap: pitch - width); positions
+// outside [lo, hi) are drawn but not stored here (other strips' columns, the r_zs interior).
 struct ChunkDest {
     long long off;
     int jump;
-    short wr;
-    signed char arr; // even: r_ys of component arr >> 1; -1: general path
-    signed char pad;
+    uint8_t wr;      // 0..128
+    signed char arr; // stream array: even r_ys, odd r_zs of component arr >> 1; -1: general path
+    uint8_t lo, hi;  // stored positions [lo, hi) of the chunk's 128
 };
 
 // Run generation (gen_dense 2): a wave generates a piece of consecutive needed 64-rank chunks [c0, c0 + n)
@@ -82,6 +83,7 @@ struct RngGeom {
     int fused_plan;                // compacted K3 plans its own waves (one GPU, nb_plan <= 1024 blocks): no K2/K2c launch
     int nb_plan;                   // attempt blocks of the call (fused_plan)
     int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
+    int end_ext;                   // run generation: K3e writes the call's end state (K3r does not; the chain runs ahead)
     int fast_log;                  // log in the polar transform: 2 glibc_log (glibc's bits), 1 log_r2 (table-driven,
                                    // within 1 ulp), 0 the device library's log (df_rng.hpp)
     const LogTabEntry *log_tab;    // kLogTab entries (build_log_table)
@@ -175,6 +177,7 @@ hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *cou
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st);
 // K2s (run generation): share `share`'s block prefix and total into its exchange record (after K1).
 hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share, hipStream_t st);
+hipError_t launch_rng_end_state(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *err, hipStream_t st);
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
                              const int *wave_counts, long long *offsets, long long *part, uint16_t *masks,
                              WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st);

@@ -1594,6 +1594,8 @@ int alloc_dense(df_handle *h)
         return true;
     };
     std::vector<ChunkDest> dest[2];
+    bool fast_partial = true;
+    if (const char *e = std::getenv("DFAMD_FAST_PARTIAL")) fast_partial = std::atoi(e) != 0;
     for (int f = 0; f < 2; ++f) {
         const long long A = (long long)((g.Q - f + 1) / 2);
         dest[f].resize(std::max<size_t>(1, list[f].size()), ChunkDest{0, 0, 0, -1, 0, 0});
@@ -1633,6 +1635,7 @@ int alloc_dense(df_handle *h)
             }
             if (!ok || lo < 0 || wraps > 1) continue;
             if (hi < 0) hi = 128;
+            if (!fast_partial && (lo != 0 || hi != 128 || (su & 1))) continue; // timing A/B: round-3 rule only
             ChunkDest d{};
             d.off = d0;
             d.jump = (int)(d1 - d0);

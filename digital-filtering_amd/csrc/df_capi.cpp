@@ -335,9 +335,6 @@ SweepArgs sweep_args(df_handle *h)
     a.zs_lo = 0;
     a.zs_n = a.zs_gap_at = h->nstrips;
     a.zs_gap = 0;
-    a.ys_lo = 0;
-    a.ys_n = a.ys_gap_at = h->nstrips;
-    a.ys_gap = 0;
     a.zgroup = 1;
     a.tab = h->tab;
     a.tab_off = h->tab_off;
@@ -806,8 +803,7 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
 {
     int lo = 0, hi = 0, rc;
     const bool peer = h->comm && !h->solo_strip; // DFAMD_SOLO_STRIP (timing only): the same streams, no exchange
-    const bool ov = h->halo_overlap > 0 || (h->halo_overlap < 0 && h->coeff_mode == DF_COEFF_PACKED); // 2 where
-    // the y-pass form does not apply: the z-pass form
+    const bool ov = h->halo_overlap > 0 || (h->halo_overlap < 0 && h->coeff_mode == DF_COEFF_PACKED);
     if (h->world == 1 || !(peer || h->solo_strip) || !ov || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
         if ((rc = phase_halo_rccl(h))) return rc;
         ev_record(h, 2);
@@ -833,69 +829,6 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     if ((rc = phase_zpass(h, corr, sra, dt, 2, h->comm_stream))) return join(rc); // edge strips
     rc = phase_zpass(h, corr, sra, dt, 1); // interior strips
     return join(rc);
-}
-
-// halo_overlap 2 (table z-strips): the exchange under the y-pass instead of the z-pass. The strips that hold
-// the columns the neighbours need (the same edge strips halo_interior names: a strip holds a sent column exactly
-// when its z stencils reach the halo) are y-filtered first on the high-priority comm_stream, which then packs,
-// exchanges and unpacks, while the stream y-filters the interior strips; the stream then joins and runs ONE
-// whole z-pass (row-grouped, LDS-staged), so nothing of the z-pass is split. Table mode's y-pass takes a strip
-// subset (SweepArgs::ys_*) only in ypass_table_kernel: the other y-pass forms keep the serial chain.
-bool yov_active(const df_handle *h, int *lo, int *hi)
-{
-    return h->halo_overlap == 2 && h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && h->comm_stream &&
-           (h->comm || h->solo_strip) && !h->group && !h->setup.per_cell && !h->ylds && h->ydepth >= 1 &&
-           halo_interior(h, lo, hi);
-}
-
-int phase_yov_zpass(df_handle *h, int lo, int hi, bool corr, bool sra, double dt)
-{
-    const bool peer = h->comm && !h->solo_strip;
-    hipStream_t cs = h->comm_stream;
-    // the stream at its y-pass: this call's noise set ready, the previous call's z-pass done with r_zs
-    HIP_OR(hipEventRecord(h->ev_packed, h->stream), DF_EHIP);
-    HIP_OR(hipStreamWaitEvent(cs, h->ev_packed, 0), DF_EHIP);
-    auto join = [h](int code) { // as phase_halo_zpass: the stream never runs ahead of comm_stream's buffers
-        if (hipEventRecord(h->ev_unpacked, h->comm_stream) == hipSuccess)
-            (void)hipStreamWaitEvent(h->stream, h->ev_unpacked, 0);
-        else
-            (void)hipStreamSynchronize(h->comm_stream);
-        return code;
-    };
-    SweepArgs a = sweep_args(h);
-    SweepArgs e = a; // edge strips [0, lo) and [hi, nstrips)
-    e.ys_lo = 0;
-    e.ys_n = lo + (h->nstrips - hi);
-    e.ys_gap_at = lo;
-    e.ys_gap = hi - lo;
-    int rc = DF_OK;
-    if (e.ys_n > 0 && launch_ypass(e, true, h->rows_per_wave, cs) != hipSuccess) rc = fail(DF_EHIP, "edge y-pass launch");
-    if (!rc && launch_halo_pack(a, h->rank > 0 ? h->send_l : nullptr, h->rank < h->world - 1 ? h->send_r : nullptr, cs) !=
-                   hipSuccess)
-        rc = fail(DF_EHIP, "halo pack launch");
-    if (!rc && peer) rc = halo_sendrecv(h, cs);
-    if (!rc && peer) rc = phase_halo_unpack(h, cs);
-    if (!rc && !peer && h->solo_xchg_us > 0 && launch_hold(h->solo_xchg_us, cs) != hipSuccess) rc = fail(DF_EHIP, "hold");
-    if (!rc && !peer && h->gen_pending && hipEventRecord(h->ev_xchg, cs) != hipSuccess) rc = fail(DF_EHIP, "ev_xchg");
-    if (rc) return join(rc);
-    SweepArgs in = a; // interior strips [lo, hi) on the stream, beside the exchange
-    in.ys_lo = lo;
-    in.ys_n = in.ys_gap_at = hi - lo;
-    if (launch_ypass(in, true, h->rows_per_wave, h->stream) != hipSuccess) return join(fail(DF_EHIP, "y-pass launch"));
-    ev_record(h, 1);
-    join(DF_OK);
-    ev_record(h, 2); // halo_ms: what of the exchange the interior y-pass did not hide
-    return phase_zpass(h, corr, sra, dt);
-}
-
-// y-pass, halo, z-pass of one visible step (phase events 1 and 2 inside)
-int phase_sweeps(df_handle *h, bool corr, bool sra, double dt)
-{
-    int lo = 0, hi = 0, rc;
-    if (yov_active(h, &lo, &hi)) return phase_yov_zpass(h, lo, hi, corr, sra, dt);
-    if ((rc = phase_ypass(h, 7))) return rc;
-    ev_record(h, 1);
-    return phase_halo_zpass(h, corr, sra, dt);
 }
 
 // part 0: every strip; 1: the halo-interior strips; 2: the edge strips around them (halo_interior)
@@ -1784,7 +1717,8 @@ int step0(df_handle *h)
     int rc;
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
-    if ((rc = phase_sweeps(h, false, false, 0.0))) return rc;
+    if ((rc = phase_ypass(h, 7))) return rc;
+    if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
     if ((rc = sync_all(h))) return rc;
     return check_rng_error(h);
@@ -1984,7 +1918,9 @@ int df_filter(df_handle *h, double dt)
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
     ev_record(h, 0);
-    if ((rc = phase_sweeps(h, true, true, dt))) return rc; // phase events 1 and 2 inside
+    if ((rc = phase_ypass(h, 7))) return rc;
+    ev_record(h, 1);
+    if ((rc = phase_halo_zpass(h, true, true, dt))) return rc; // phase event 2 inside
     ev_record(h, 3);
     if ((rc = prefetch_gen(h))) return rc; // next call's noise, under this call's sweeps
     if (prof) h->ev_used++;
@@ -2363,7 +2299,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
-        h->halo_overlap = value < 0 ? -1 : value > 2 ? 2 : value;
+        h->halo_overlap = value < 0 ? -1 : value != 0;
     }
 
     else if (k == "ycoop_order") {

@@ -1797,10 +1797,9 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
     const int per_xcd = gridDim.x >> 3; // XCD-aware order, as ypass_kernel
     const int b = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
     const int tile = uniform(b * 4 + (threadIdx.x >> 6));
-    if (tile >= a.ys_n * nrowblk) return; // this launch's strips (SweepArgs::ys_lo ...)
-    const int sl = tile / nrowblk;
-    const int s = a.ys_lo + sl + (sl >= a.ys_gap_at ? a.ys_gap : 0);
-    const int rb = nrowblk - 1 - (tile - sl * nrowblk); // wide stencils (large j) start first
+    if (tile >= a.nstrips * nrowblk) return;
+    const int s = tile / nrowblk;
+    const int rb = nrowblk - 1 - (tile - s * nrowblk); // wide stencils (large j) start first
     const int j0 = rb * R;
     const int Ny = a.Ny;
     const int nr = min(R, Ny - j0);
@@ -2240,7 +2239,6 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 {
     if constexpr (TABLE) {
         if (a.ylds && !a.per_cell) {
-            if (a.ys_lo != 0 || a.ys_n != a.nstrips || a.ys_gap != 0) return hipErrorInvalidValue;
             const int nrowblk = (a.Ny + 4 * R - 1) / (4 * R);
             const unsigned blocks = (unsigned)(((long long)a.nstrips * nrowblk + 7) / 8 * 8);
             // 4 and 8 rows per wave take one chunk in flight: with 2-3 the compiler puts their arrays in scratch
@@ -2250,10 +2248,7 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
         }
     }
     const int nrowblk = (a.Ny + R - 1) / R;
-    // ypass_table_kernel takes a strip subset (ys_*); the other forms always run the whole plane
-    const bool sub = TABLE && !a.per_cell && a.ydepth >= 1;
-    if (!sub && (a.ys_lo != 0 || a.ys_n != a.nstrips || a.ys_gap != 0)) return hipErrorInvalidValue;
-    const long long tiles = (long long)(sub ? a.ys_n : a.nstrips) * nrowblk;
+    const long long tiles = (long long)a.nstrips * nrowblk;
     const unsigned blocks = (unsigned)(((tiles + 3) / 4 + 7) / 8 * 8); // multiple of 8 for the XCD swizzle
     const dim3 grid(blocks, 3);
     if constexpr (TABLE) {
@@ -2281,7 +2276,6 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
 hipError_t launch_ypass(const SweepArgs &a, bool table, int rows_per_wave, hipStream_t st)
 {
     if (!table && a.ycoop >= 7) { // row pairs, 4 noise rows per wave per chunk (32 KiB LDS)
-        if (a.ys_lo != 0 || a.ys_n != a.nstrips || a.ys_gap != 0) return hipErrorInvalidValue;
         const dim3 grid((unsigned)(8 * a.ycoop2_run), 3);
         hipLaunchKernelGGL((ypass_coop2_kernel<true, 4>), grid, dim3(256), 0, st, a);
         return hipGetLastError();

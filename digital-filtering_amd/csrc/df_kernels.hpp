@@ -155,7 +155,6 @@ struct SweepArgs {
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.
     int zs_lo, zs_n, zs_gap_at, zs_gap;
-    int ys_lo, ys_n, ys_gap_at, ys_gap; // the same for the table y-pass (ypass_table_kernel; halo_overlap 2)
     int zgroup;             // table z-pass: blocks of (row, <= 4 consecutive strips) (launches without a gap)
     int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
     int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead

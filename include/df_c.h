@@ -226,8 +226,7 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   the call's halo group, one grouped RCCL operation per call; 0 = an all-gather of their own),
  *   "rng_replicate" (z-strips: 1 every rank counts every attempt, 0 split counting), "halo_overlap"
  *   (RCCL z-strips: 1 = send/recv, unpack and edge-strip z-pass on a high-priority stream under the
- *   interior strips' z-pass; 2 = table mode: the edge strips' y-pass, pack, send/recv and unpack on that
- *   stream under the interior strips' y-pass, then one whole z-pass; 0 = one serial chain; -1 default), "halo_loopback"
+ *   interior strips' z-pass; 0 = one serial chain; -1 default = 1 packed, 0 table), "halo_loopback"
  *   (one-rank RCCL handle: send the halo to itself and check it), "fast_log" (above). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 

@@ -96,12 +96,10 @@ def test_rccl_strips_emulated_hosts(world, mode, replicate):
 
 @pytest.mark.parametrize("world,Nz", [(2, 1024), (3, 1000), (4, 2048)])
 @pytest.mark.parametrize("mode,replicate", [("packed", 1), ("table", 0)])
-@pytest.mark.parametrize("overlap", [0, 1, 2])
+@pytest.mark.parametrize("overlap", [0, 1])
 def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
-    """Every halo form bit-equal to the unsplit plane: the exchange under the interior strips' z-pass
-    (halo_overlap 1; N_max 64 leaves 1-3 interior strips per rank here), under the interior strips' y-pass
-    with the edge strips y-filtered first on the comm stream (2; table mode, packed falls back to 1) and the
-    serial chain (0)."""
+    """Both halo forms bit-equal to the unsplit plane: the exchange under the interior strips' z-pass (the
+    default; N_max 64 leaves 1-3 interior strips per rank here) and the serial chain (halo_overlap 0)."""
     if n_gpus() < 1:
         pytest.skip("needs a GPU")
     outs = run_world(world, mode, replicate, Nz=Nz, N_min=4, N_max=64, emulate=True,
@@ -109,7 +107,7 @@ def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
     check_world(outs, world, replicate, Nz=Nz)
 
 
-@pytest.mark.parametrize("mode,replicate,tuning", [("packed", 1, {}), ("table", 0, {}), ("table", 0, {"halo_overlap": 2})])
+@pytest.mark.parametrize("mode,replicate,tuning", [("packed", 1, {}), ("table", 0, {}), ("table", 0, {"gen_dense": 2})])
 def test_rccl_c4_real_partition_emulated(mode, replicate, tuning):
     """The partition the driver's 8-GPU bench runs first: BASELINE configs[3] (c4,
     2048 x 8192, N 4-64) in eight 2048 x 1024 strips, each rank's 3.1 MB halos per side through the

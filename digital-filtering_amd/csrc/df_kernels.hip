@@ -2631,11 +2631,14 @@ __global__ void halo_pack_kernel(SweepArgs a, double *__restrict__ sl, double *_
         const size_t n = (size_t)a.Ny * W;
         for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
             const int j = (int)(e / W), kk = (int)(e - (size_t)j * W);
+            const int w = a.halo_w[c] ? a.halo_w[c][j] : W;
+            if (kk >= w) continue;
+            const size_t o = base + (a.halo_w[c] ? (size_t)a.halo_off[c][j] : (size_t)j * W) + kk;
             const double *row = a.rz[c] + (size_t)j * a.rz_pitch[c] + a.Nzp[c];
-            if (sl) sl[base + e] = row[kk];
-            if (sr) sr[base + e] = row[a.Nz_loc - W + kk];
+            if (sl) sl[o] = row[kk];              // to rank - 1: this strip's first w columns
+            if (sr) sr[o] = row[a.Nz_loc - w + kk]; // to rank + 1: its last w
         }
-        base += n;
+        base += a.halo_w[c] ? (size_t)a.halo_off[c][a.Ny] : n;
     }
 }
 
@@ -2647,11 +2650,14 @@ __global__ void halo_unpack_kernel(SweepArgs a, const double *__restrict__ rl, c
         const size_t n = (size_t)a.Ny * W;
         for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < n; e += (size_t)gridDim.x * blockDim.x) {
             const int j = (int)(e / W), kk = (int)(e - (size_t)j * W);
+            const int w = a.halo_w[c] ? a.halo_w[c][j] : W;
+            if (kk >= w) continue;
+            const size_t o = base + (a.halo_w[c] ? (size_t)a.halo_off[c][j] : (size_t)j * W) + kk;
             double *row = a.rz[c] + (size_t)j * a.rz_pitch[c];
-            if (rl) row[kk] = rl[base + e];
-            if (rr) row[a.Nzp[c] + a.Nz_loc + kk] = rr[base + e];
+            if (rl) row[W - w + kk] = rl[o];              // left pad: the w columns just left of the strip
+            if (rr) row[a.Nzp[c] + a.Nz_loc + kk] = rr[o]; // right pad: the w columns just right of it
         }
-        base += n;
+        base += a.halo_w[c] ? (size_t)a.halo_off[c][a.Ny] : n;
     }
 }
 

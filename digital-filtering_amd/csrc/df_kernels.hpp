@@ -154,6 +154,10 @@ struct SweepArgs {
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.
     int zs_lo, zs_n, zs_gap_at, zs_gap;
+    // z-halo of row j, component c: the plane's widest z half-width of that row (Setup Nz_row, the same on every
+    // rank) columns, packed row after row at halo_off[c][j] (nullptr: Nzp[c] columns for every row)
+    const int *halo_w[3];
+    const long long *halo_off[3];
     int zgroup;             // table z-pass: blocks of (row, <= 4 consecutive strips) (launches without a gap)
     int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
     int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead

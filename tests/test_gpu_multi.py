@@ -119,8 +119,16 @@ def test_rccl_c4_real_partition_emulated(mode, replicate, tuning):
                      extra=dict(tuning=tuning))
     check_world(outs, 8, replicate, Nz=8192)
     assert sorted(o["columns"] for o in outs) == [[r * 1024, (r + 1) * 1024] for r in range(8)]
+    # the halo of row j carries that row's widest z half-width (not N_max) columns per side
+    import numpy as np
+    import dfamd
+    host = dfamd.DigitalFilter(plane="synthetic", Ny=2048, Nz=8192, N_min=4, N_max=64, seed=11, device=-1,
+                               coeff_mode=mode)
+    per_side = 8 * sum(int(np.minimum(host.halfwidths(c, "z").max(axis=1), host.comp_info(c)["Nz_max"]).sum())
+                       for c in range(3))
+    assert per_side < 2048 * 64 * 3 * 8
     for o in outs:
-        assert o["comm"]["halo_bytes_sent"] == o["comm"]["halo_peers"] * 2048 * 64 * 3 * 8, o["comm"]
+        assert o["comm"]["halo_bytes_sent"] == o["comm"]["halo_peers"] * per_side, (o["comm"], per_side)
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])

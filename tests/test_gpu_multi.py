@@ -110,7 +110,7 @@ def test_rccl_halo_overlap_forms_emulated(world, Nz, mode, replicate, overlap):
 @pytest.mark.parametrize("mode,replicate,tuning", [("packed", 1, {}), ("table", 0, {}), ("table", 0, {"gen_dense": 2})])
 def test_rccl_c4_real_partition_emulated(mode, replicate, tuning):
     """The partition the driver's 8-GPU bench runs first: BASELINE configs[3] (c4,
-    2048 x 8192, N 4-64) in eight 2048 x 1024 strips, each rank's 3.1 MB halos per side through the
+    2048 x 8192, N 4-64) in eight 2048 x 1024 strips, each rank's 2.5 MB halos per side through the
     product's grouped ncclSend/ncclRecv (RCCL socket transport between emulated hosts on one GPU), every
     strip bit-equal to the whole plane run unsplit after step 0 and two calls."""
     if n_gpus() < 1:

@@ -183,21 +183,6 @@ struct df_handle {
     // edge launch runs unstaged, against an exchange of a few tens of us).
     int halo_overlap = -1;
     hipStream_t comm_stream = nullptr;
-    // Table z-strips with the fused exchange (round 4): K3r on a stream of its own, behind K3e, which writes the
-    // generation's end state right after the exchange - so the next generation's count never waits for this
-    // one's generation (the state chain is K1 -> exchange -> K3e only). Records double-buffered by generation.
-    hipStream_t gen_stream = nullptr;
-    hipEvent_t ev_state = nullptr, ev_k3r_done[2] = {nullptr, nullptr};
-    size_t xhalf = 0; // bytes of one record buffer when double-buffered (0: one buffer)
-    int decouple = 1; // DFAMD_GEN_DECOUPLE (timing A/B): 0 keeps K3r on rng_stream, writing the end state itself
-    // Where K3r of the generation counted last goes (DFAMD_K3R_AT): 0 right after its K3e (the end of the call
-    // that exchanged its records), 1 at the start of the next call, 2 after that call's y-pass - so that its
-    // work is still there to fill the SIMDs while the call waits for its halo
-    int k3r_at = 1;
-    bool k3r_pending = false;
-    RngGeom k3r_g{};
-    long long k3r_gi = 0;
-    hipEvent_t ev_ypass = nullptr;
     hipEvent_t ev_packed = nullptr, ev_unpacked = nullptr; // halo packed (stream); edge strips done (comm_stream)
     std::shared_ptr<std::vector<df_handle *>> group; // in-process strip group (df_create_group)
     long long gen_launched = 0; // generations enqueued (generation n reads state slot n%nsets, writes (n+1)%nsets)
@@ -436,14 +421,11 @@ void ev_record(df_handle *h, int phase, hipStream_t st = nullptr)
     (void)hipEventRecord(h->ev[h->ev_used].e[phase], st ? st : phase >= 4 && h->overlap ? h->rng_stream : h->stream);
 }
 
-int flush_k3r(df_handle *h, hipEvent_t after);
 int sync_all(df_handle *h)
 {
-    if (int rc = flush_k3r(h, nullptr)) return rc;
     HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     if (h->comm_stream) HIP_OR(hipStreamSynchronize(h->comm_stream), DF_EHIP);
-    if (h->gen_stream) HIP_OR(hipStreamSynchronize(h->gen_stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -502,15 +484,12 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
         HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e & 1], 0), DF_EHIP);
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
-    g.end_ext = 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
     g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? h->gen_dense : 0;
     if (g.gen_dense == 2) { // K1 writes the group counts of its share's record, K2s the share's prefix
-        g.xbuf = h->xbuf + (h->xhalf ? (size_t)(gi & 1) * h->xhalf : 0);
-        // double-buffered records: the K3r of generation gi - 2 (gen_stream) read this buffer last
-        if (h->xhalf && h->gen_stream) HIP_OR(hipStreamWaitEvent(rs, h->ev_k3r_done[gi & 1], 0), DF_EHIP);
+        g.xbuf = h->xbuf;
         g.xworld = h->split_count ? h->world : 1;
         g.xchunk = h->split_count ? h->rng_chunk : h->rng_blocks;
         record_layout(g.xchunk, &g.xstride, &g.xlp_off, &g.xtot_off);
@@ -540,9 +519,9 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
 
 int phase_ypass(df_handle *h, int comps_mask);
 
-// K3r (or the whole finish of a non-run form) of generation gi on rs, and the events that follow it.
-int gen_finish(df_handle *h, const RngGeom &g, hipStream_t rs, long long gi)
+int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
+    const long long gi = h->gen_launched;
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
     // split counting exchanges counts only: K3 recomputes the accept flags of the waves it runs
     // (g.recount), a sixth or less of all waves on an interior rank of 8
@@ -553,24 +532,8 @@ int gen_finish(df_handle *h, const RngGeom &g, hipStream_t rs, long long gi)
     if (prof_on(h)) ev_record(h, 5, rs);
     if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
-    if (h->xhalf && h->gen_stream && g.gen_dense == 2) HIP_OR(hipEventRecord(h->ev_k3r_done[gi & 1], rs), DF_EHIP);
+    h->gen_launched++;
     return DF_OK;
-}
-
-int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
-{
-    int rc = gen_finish(h, g, rs, h->gen_launched);
-    if (!rc) h->gen_launched++;
-    return rc;
-}
-
-// Launch a K3r deferred by fused_gen_end (k3r_at > 0) on gen_stream, after `after` if given.
-int flush_k3r(df_handle *h, hipEvent_t after = nullptr)
-{
-    if (!h->k3r_pending) return DF_OK;
-    h->k3r_pending = false;
-    if (after) HIP_OR(hipStreamWaitEvent(h->gen_stream, after, 0), DF_EHIP);
-    return gen_finish(h, h->k3r_g, h->gen_stream, h->k3r_gi);
 }
 
 // In-process strip group: every member counts its share, the shares are copied
@@ -662,7 +625,6 @@ int consume_gen(df_handle *h)
     const long long gi = h->gen_used, e = gen_epoch(h, gi);
     const bool first = gen_pos(h, gi) == 0;
     int rc;
-    if (h->k3r_pending && h->k3r_gi <= gi && (rc = flush_k3r(h))) return rc;
     // DFAMD_ABLATE_HANDOFF (timing only, wrong results possible): 1 no wait for the noise, 2 no release
     if (first && gi > (h->hb == 1 ? 0 : h->gen_base) && !(h->ablate_handoff & 2))
         HIP_OR(hipEventRecord(h->ev_release[(e - 1) & 1], h->stream), DF_EHIP); // the previous epoch's sets free
@@ -728,20 +690,7 @@ int fused_gen_end(df_handle *h)
         HIP_OR(hipStreamWaitEvent(rs, h->ev_xchg, 0), DF_EHIP);
         HIP_OR(launch_replicate_share(h->pend_g.xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
     }
-    if (!h->gen_stream || !h->decouple) return gen_end(h, h->pend_g, rs);
-    // K3e: the end state (next generation's start) right after the exchange, on rng_stream; K3r on gen_stream
-    const long long gi = h->gen_launched;
-    HIP_OR(launch_rng_end_state(h->pend_g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->err_dev, rs),
-           DF_EHIP);
-    HIP_OR(hipEventRecord(h->ev_state, rs), DF_EHIP);
-    HIP_OR(hipStreamWaitEvent(h->gen_stream, h->ev_state, 0), DF_EHIP);
-    h->pend_g.end_ext = 1;
-    if (h->k3r_at == 0) return gen_end(h, h->pend_g, h->gen_stream);
-    if (prof_on(h)) ev_record(h, 5, rs); // rng_ms then spans K1 .. K3e of the generation
-    h->k3r_g = h->pend_g;
-    h->k3r_gi = h->gen_launched++;
-    h->k3r_pending = true;
-    return DF_OK;
+    return gen_end(h, h->pend_g, rs);
 }
 
 int phase_ypass(df_handle *h, int comps_mask)
@@ -1448,10 +1397,7 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         long long st1 = 0, stw = 0, lo, to;
         record_layout(h->rng_blocks, &st1, &lo, &to);
         record_layout(h->rng_chunk, &stw, &lo, &to);
-        const size_t xb = (size_t)std::max(st1, stw * h->world);
-        // table z-strips: two record buffers (generation parity), so K3r may run behind the next generation's K1
-        h->xhalf = h->world > 1 && h->coeff_mode == DF_COEFF_TABLE ? (xb + 255) / 256 * 256 : 0;
-        if ((rc = dalloc_t(h, &h->xbuf, h->xhalf ? 2 * h->xhalf : xb))) return rc;
+        if ((rc = dalloc_t(h, &h->xbuf, (size_t)std::max(st1, stw * h->world)))) return rc;
         if (h->world > 64) return fail(DF_EINVAL, "more than 64 z-strip ranks"); // run generation's share lookup
     }
     h->geom.nb_groups = (long long)h->rng_blocks * 64;
@@ -1697,14 +1643,6 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         int prio_lo = 0, prio_hi = 0;
         HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
         HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
-        if (h->xhalf && h->overlap) {
-            HIP_OR(hipStreamCreateWithFlags(&h->gen_stream, hipStreamNonBlocking), DF_EHIP);
-            HIP_OR(hipEventCreateWithFlags(&h->ev_state, hipEventDisableTiming), DF_EHIP);
-            for (auto &e : h->ev_k3r_done) HIP_OR(hipEventCreateWithFlags(&e, hipEventDisableTiming), DF_EHIP);
-            if (const char *e = std::getenv("DFAMD_GEN_DECOUPLE")) h->decouple = std::atoi(e);
-            if (const char *e = std::getenv("DFAMD_K3R_AT")) h->k3r_at = std::atoi(e);
-            HIP_OR(hipEventCreateWithFlags(&h->ev_ypass, hipEventDisableTiming), DF_EHIP);
-        }
         HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_xchg, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
@@ -1765,26 +1703,13 @@ int build(df_handle *h, const df_config_c *cfg)
     return DF_OK;
 }
 
-// The deferred K3r (k3r_at): at the call's start (1) or after its y-pass (2).
-int place_k3r(df_handle *h, int at)
-{
-    if (!h->k3r_pending || h->k3r_at != at) return DF_OK;
-    if (at == 2) {
-        HIP_OR(hipEventRecord(h->ev_ypass, h->stream), DF_EHIP);
-        return flush_k3r(h, h->ev_ypass);
-    }
-    return flush_k3r(h, nullptr);
-}
-
 int step0(df_handle *h)
 {
     // Constructor step 0 (df.cpp:57-62): noise, sweeps, RST; no correlation, no SRA.
     int rc;
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
-    if ((rc = place_k3r(h, 1))) return rc;
     if ((rc = phase_ypass(h, 7))) return rc;
-    if ((rc = place_k3r(h, 2))) return rc;
     if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
     if ((rc = sync_all(h))) return rc;
@@ -1799,7 +1724,6 @@ void destroy(df_handle *h)
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
-    if (h->gen_stream) (void)hipStreamSynchronize(h->gen_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
     for (void *p : h->allocs) {
@@ -1817,11 +1741,6 @@ void destroy(df_handle *h)
     }
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
-    if (h->gen_stream) (void)hipStreamDestroy(h->gen_stream);
-    if (h->ev_state) (void)hipEventDestroy(h->ev_state);
-    if (h->ev_ypass) (void)hipEventDestroy(h->ev_ypass);
-    for (auto &e : h->ev_k3r_done)
-        if (e) (void)hipEventDestroy(e);
     if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
     if (h->ev_xchg) (void)hipEventDestroy(h->ev_xchg);
     if (h->ev_unpacked) (void)hipEventDestroy(h->ev_unpacked);
@@ -1985,10 +1904,8 @@ int df_filter(df_handle *h, double dt)
     const bool prof = prof_on(h);
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
-    if ((rc = place_k3r(h, 1))) return rc;
     ev_record(h, 0);
     if ((rc = phase_ypass(h, 7))) return rc;
-    if ((rc = place_k3r(h, 2))) return rc;
     ev_record(h, 1);
     if ((rc = phase_halo_zpass(h, true, true, dt))) return rc; // phase event 2 inside
     ev_record(h, 3);

@@ -864,7 +864,7 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
             const double xm = a.x * mult;
             const double ym = a.y * mult;
             store_pair(g, d0, d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
-            if (last && !g.end_ext) { // (K3e writes it when the generation runs behind the state chain)
+            if (last) {
                 sout->state = s3 * kPcgMult + kPcgInc; // state after this attempt's 4th output
                 sout->saved_flag = (int)((g.Q - f) & 1u);
                 sout->saved = xm;
@@ -1118,57 +1118,6 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
         __asm__ volatile("" ::: "memory");
         near1_batch(g, stk, top, top, lane);
     }
-}
-
-// K3e: the call's end state alone, one wave, from the share records: locate rank A - 1 (the call's last accepted
-// attempt), redo its exact accept test across its group (the same decisions as K1's screen), and write what
-// K3r's last chunk writes - the state after that attempt's fourth output, the parity of the carried normal and
-// the attempt's x normal (df.cpp:332-349 through random.tcc:1800-1835). With it the next generation's count
-// (K1) depends on this one's exchange only, not on its generation: K3r leaves the state chain.
-__global__ __launch_bounds__(64) void rng_end_state_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                           RngStateDev *__restrict__ sout, int *__restrict__ err)
-{
-    const int lane = threadIdx.x;
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    long long G, grand;
-    int skip;
-    const bool found = locate_rank(g, A - 1, lane, G, skip, grand);
-    if (grand < A) {
-        if (lane == 0) *err = 1; // not enough attempts launched: the host re-sizes
-        return;
-    }
-    if (!found) return;
-    G = uniform((int)G);
-    const uint64_t S = sin->state;
-    const PcgJumpDev jb = g.jump_block[G >> 6], jg = g.jump_gi[G & 63], jl = g.jump_lane[lane];
-    const uint64_t s0 = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
-    uint64_t st = s0; // polar_attempt advances its argument
-    const bool acc = polar_attempt(st).accept;
-    const uint64_t m = __ballot(acc);
-    const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (!acc || below != uniform(skip)) return;
-    PolarAttempt a{};
-    uint64_t s3 = s0;
-    if (g.debug_flags & 4) { // timing ablation, as dense_chunk
-        a.x = (double)(uint32_t)s0 * 1e-10;
-        a.y = 0.5;
-        a.r2 = 0.5;
-    } else {
-        a = polar_draws(s0, s3);
-    }
-    const double lg = g.fast_log == 2 ? glibc_log(a.r2) : polar_log(g, a.r2);
-    const double mult = (g.debug_flags & 1) ? a.r2 : sqrt(-2 * lg / a.r2);
-    const double xm = a.x * mult;
-    sout->state = s3 * kPcgMult + kPcgInc;
-    sout->saved_flag = (int)((g.Q - f) & 1u);
-    sout->saved = xm;
-}
-
-hipError_t launch_rng_end_state(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *err, hipStream_t st)
-{
-    hipLaunchKernelGGL(rng_end_state_kernel, dim3(1), dim3(64), 0, st, g, st_in, st_out, err);
-    return hipGetLastError();
 }
 
 // K2 + K2c in one block for planes of at most 1024 attempt blocks (c1, c2, the reference's own

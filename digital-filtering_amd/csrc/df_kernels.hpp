@@ -83,7 +83,6 @@ struct RngGeom {
     int fused_plan;                // compacted K3 plans its own waves (one GPU, nb_plan <= 1024 blocks): no K2/K2c launch
     int nb_plan;                   // attempt blocks of the call (fused_plan)
     int recount;                   // split counting: K3 recomputes its waves' accept flags (masks are not exchanged)
-    int end_ext;                   // run generation: K3e writes the call's end state (K3r does not; the chain runs ahead)
     int fast_log;                  // log in the polar transform: 2 glibc_log (glibc's bits), 1 log_r2 (table-driven,
                                    // within 1 ulp), 0 the device library's log (df_rng.hpp)
     const LogTabEntry *log_tab;    // kLogTab entries (build_log_table)
@@ -180,7 +179,6 @@ hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *cou
                             uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st);
 // K2s (run generation): share `share`'s block prefix and total into its exchange record (after K1).
 hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share, hipStream_t st);
-hipError_t launch_rng_end_state(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *err, hipStream_t st);
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,
                              const int *wave_counts, long long *offsets, long long *part, uint16_t *masks,
                              WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st);

@@ -1599,8 +1599,6 @@ int alloc_dense(df_handle *h)
     // of near-equal length within a run (a 9-chunk row segment of a strip is one piece, not 8 + 1)
     uint32_t kRunPiece = 12;
     if (const char *e = std::getenv("DFAMD_RUN_PIECE")) kRunPiece = (uint32_t)std::max(1, std::atoi(e));
-    bool merge_pieces = true; // DFAMD_MERGE_PIECES=0 (timing A/B): one piece per wave
-    if (const char *e = std::getenv("DFAMD_MERGE_PIECES")) merge_pieces = std::atoi(e) != 0;
     for (int f = 0; f < 2; ++f) {
         std::vector<RunPiece> pcs;
         const std::vector<uint32_t> &L = list[f];
@@ -1621,23 +1619,6 @@ int alloc_dense(df_handle *h)
         if (!pcs.empty() && (rc = upload(h, dp, pcs.data(), pcs.size()))) return rc;
         h->geom.pieces[f] = dp;
         h->geom.npieces[f] = (int)pcs.size();
-        // waves: consecutive pieces while they total at most kRunPiece chunks (at most 8 pieces: each one costs a
-        // locate), so the short pad pieces share a wave instead of paying a wave and a near-1 batch each
-        std::vector<int> wp{0};
-        for (size_t q = 0, tot = 0; q < pcs.size(); ++q) {
-            const bool fits = tot + pcs[q].n <= kRunPiece && (int)q - wp.back() < (merge_pieces ? 8 : 1);
-            if (q > (size_t)wp.back() && !fits) {
-                wp.push_back((int)q);
-                tot = 0;
-            }
-            tot += pcs[q].n;
-        }
-        wp.push_back((int)pcs.size());
-        int *dw = nullptr;
-        if ((rc = dalloc_t(h, &dw, wp.size()))) return rc;
-        if ((rc = upload(h, dw, wp.data(), wp.size()))) return rc;
-        h->geom.wave_piece[f] = dw;
-        h->geom.nwaves[f] = (int)wp.size() - 1;
     }
     return DF_OK;
 }

@@ -1046,79 +1046,74 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
         double *d = stream_dest(g, stream_pos(g, 0));
         if (d) *d = sin->saved * 1.0 + 0.0;
     }
-    if (p >= g.nwaves[f]) return;
+    if (p >= g.npieces[f]) return;
+    const RunPiece pc = g.pieces[f][p];
     const bool defer = g.fast_log == 2;
+    const long long c0 = uniform((int)pc.c0), cend = c0 + uniform((int)pc.n);
+    long long G, grand;
+    int skip;
+    const bool found = locate_rank(g, c0 * 64, lane, G, skip, grand);
+    if (p == g.npieces[f] - 1 && lane == 0 && grand < A) *err = 1; // not enough attempts launched: host re-sizes
+    if (!found) return;
+    G = uniform((int)G);
+    long long R = c0 * 64 - uniform(skip); // rank of group G's first accepted attempt
+    const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
+    // lane's attempt 64 G + lane: its start state s0 (RECOUNT: s1, 1 step on, and s3, 3 steps on, instead)
+    uint64_t st, s3 = 0;
+    {
+        const uint64_t S = sin->state;
+        const PcgJumpDev jb = g.jump_block[G >> 6], jg = g.jump_gi[G & 63], jl = g.jump_lane[lane];
+        st = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
+        if (RECOUNT) {
+            st = st * kPcgMult + kPcgInc;
+            s3 = st * kPcgMult2 + kPcgInc2;
+        }
+    }
+    const long long nwords = g.nb_groups >> 4; // mask words per lane in the call
+    uint32_t mw = 0, mw_next = 0;
+    if (!RECOUNT) {
+        mw = masks[(size_t)(G >> 4) * 64 + lane];
+        mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
+    }
+    long long c = c0;
     int top = 0;
-    // the wave's pieces [wave_piece[p], wave_piece[p + 1]): one run of up to 12 chunks, or several short ones
-    // (a strip's raw-noise pads, 1-2 chunks a row) sharing the wave, its near-1 stack and its final batch
-    const int q0 = uniform(g.wave_piece[f][p]), q1 = uniform(g.wave_piece[f][p + 1]);
-    for (int q = q0; q < q1; ++q) {
-        const RunPiece pc = g.pieces[f][q];
-        const long long c0 = uniform((int)pc.c0), cend = c0 + uniform((int)pc.n);
-        long long G, grand;
-        int skip;
-        const bool found = locate_rank(g, c0 * 64, lane, G, skip, grand);
-        if (q == g.npieces[f] - 1 && lane == 0 && grand < A) *err = 1; // not enough attempts launched: host re-sizes
-        if (!found) continue;
-        G = uniform((int)G);
-        long long R = c0 * 64 - uniform(skip); // rank of group G's first accepted attempt
-        const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
-        // lane's attempt 64 G + lane: its start state s0 (RECOUNT: s1, 1 step on, and s3, 3 steps on, instead)
-        uint64_t st, s3 = 0;
-        {
-            const uint64_t S = sin->state;
-            const PcgJumpDev jb = g.jump_block[G >> 6], jg = g.jump_gi[G & 63], jl = g.jump_lane[lane];
-            st = jl.mult * (jg.mult * (jb.mult * S + jb.plus) + jg.plus) + jl.plus;
-            if (RECOUNT) {
-                st = st * kPcgMult + kPcgInc;
-                s3 = st * kPcgMult2 + kPcgInc2;
+    while (c < cend && G < g.nb_groups) { // uniform; the group bound only matters after a shortage (err set)
+        bool acc;
+        if (RECOUNT) {
+            const int v = polar_screen13(st, s3);
+            acc = v > 0;
+            if (v < 0) { // ~2e-5 of the attempts: the exact double test (random.tcc:1822-1826), as K1
+                uint64_t s0 = (st - kPcgInc) * kPcgMultInv;
+                acc = polar_attempt(s0).accept;
+            }
+        } else {
+            acc = (mw >> (G & 15)) & 1u;
+        }
+        const uint64_t m = __ballot(acc);
+        const long long rank = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = st;
+        R += __popcll(m);
+        ++G;
+        if (RECOUNT) {
+            st = g.next_mult * st + g.next_plus1;
+            s3 = g.next_mult * s3 + g.next_plus3;
+        } else {
+            st = g.next_mult * st + g.next_plus;
+            if ((G & 15) == 0) { // the next (block, wave) word; the one after it in flight
+                mw = mw_next;
+                mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
             }
         }
-        const long long nwords = g.nb_groups >> 4; // mask words per lane in the call
-        uint32_t mw = 0, mw_next = 0;
-        if (!RECOUNT) {
-            mw = masks[(size_t)(G >> 4) * 64 + lane];
-            mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
+        __asm__ volatile("" ::: "memory"); // wave-private ring: only the compiler must keep the order
+        while (c < cend && R >= min((c + 1) * 64, A)) { // every rank of chunk c is in the ring
+            const uint64_t rs = ring[(c * 64 + lane) & 127];
+            const uint64_t s = RECOUNT ? (rs - kPcgInc) * kPcgMultInv : rs;
+            dense_chunk(g, f, A, c, (int)pc.li0 + (int)(c - c0), s, lane, defer, stk, top, sout);
+            ++c;
         }
-        long long c = c0;
-        while (c < cend && G < g.nb_groups) { // uniform; the group bound only matters after a shortage (err set)
-            bool acc;
-            if (RECOUNT) {
-                const int v = polar_screen13(st, s3);
-                acc = v > 0;
-                if (v < 0) { // ~2e-5 of the attempts: the exact double test (random.tcc:1822-1826), as K1
-                    uint64_t s0 = (st - kPcgInc) * kPcgMultInv;
-                    acc = polar_attempt(s0).accept;
-                }
-            } else {
-                acc = (mw >> (G & 15)) & 1u;
-            }
-            const uint64_t m = __ballot(acc);
-            const long long rank = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = st;
-            R += __popcll(m);
-            ++G;
-            if (RECOUNT) {
-                st = g.next_mult * st + g.next_plus1;
-                s3 = g.next_mult * s3 + g.next_plus3;
-            } else {
-                st = g.next_mult * st + g.next_plus;
-                if ((G & 15) == 0) { // the next (block, wave) word; the one after it in flight
-                    mw = mw_next;
-                    mw_next = (G >> 4) + 1 < nwords ? masks[(size_t)((G >> 4) + 1) * 64 + lane] : 0u;
-                }
-            }
-            __asm__ volatile("" ::: "memory"); // wave-private ring: only the compiler must keep the order
-            while (c < cend && R >= min((c + 1) * 64, A)) { // every rank of chunk c is in the ring
-                const uint64_t rs = ring[(c * 64 + lane) & 127];
-                const uint64_t s = RECOUNT ? (rs - kPcgInc) * kPcgMultInv : rs;
-                dense_chunk(g, f, A, c, (int)pc.li0 + (int)(c - c0), s, lane, defer, stk, top, sout);
-                ++c;
-            }
-            __asm__ volatile("" ::: "memory");
-        }
-    } // pieces of the wave
+        __asm__ volatile("" ::: "memory");
+    }
     if (top > 0) {
         __asm__ volatile("" ::: "memory");
         near1_batch(g, stk, top, top, lane);
@@ -1236,7 +1231,7 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
     constexpr bool small_ok = true;
 #endif
     if (g.gen_dense == 2) { // run generation: K3r alone (K2s ran with K1, before any exchange)
-        const int np = g.nwaves[0] > g.nwaves[1] ? g.nwaves[0] : g.nwaves[1];
+        const int np = g.npieces[0] > g.npieces[1] ? g.npieces[0] : g.npieces[1];
         if (g.recount)
             hipLaunchKernelGGL(rng_run_generate_kernel<true>, dim3((np + 3) / 4), dim3(kRngThreads), 0, st, g, st_in,
                                st_out, masks, err);

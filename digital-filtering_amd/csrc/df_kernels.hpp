@@ -111,8 +111,6 @@ struct RngGeom {
     int xchunk, xworld;
     const RunPiece *pieces[2];
     int npieces[2];
-    const int *wave_piece[2]; // K3r wave w takes pieces [wave_piece[f][w], wave_piece[f][w + 1])
-    int nwaves[2];
     const PcgJumpDev *jump_gi, *jump_lane;
     long long nb_groups; // groups of the call's attempt blocks (64 per block)
 };

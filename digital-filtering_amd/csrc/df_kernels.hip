@@ -771,7 +771,7 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
                                             int lane, bool defer, Near1Slot *stk, int &top,
                                             RngStateDev *__restrict__ sout)
 {
-    const ChunkDest cd = g.chunk_dest[f] && !g.debug_flags ? g.chunk_dest[f][di] : ChunkDest{0, 0, 0, -1, 0, 0};
+    const ChunkDest cd = g.chunk_dest[f] ? g.chunk_dest[f][di] : ChunkDest{0, 0, 0, -1, 0, 0};
     if (cd.arr >= 0) { // uniform
         // fast chunk (host-built ChunkDest): no lane is past the call or its last attempt, the stored positions
         // are one run [lo, hi) in one stream array with at most one row wrap - no stream position search
@@ -783,9 +783,16 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
         double *const p0 = e0 >= cd.lo && e0 < cd.hi ? base + e0 + (e0 >= cd.wr ? cd.jump : 0) : nullptr;
         double *const p1 = e1 >= cd.lo && e1 < cd.hi ? base + e1 + (e1 >= cd.wr ? cd.jump : 0) : nullptr;
         const bool livef = p0 || p1;
-        uint64_t s3f;
-        const PolarAttempt af = polar_draws(s, s3f);
-        const bool nearf = defer && livef && glibc_log_near1(af.r2);
+        uint64_t s3f = s;
+        PolarAttempt af{};
+        if (g.debug_flags & 4) { // timing ablations only, as the general path below
+            af.x = (double)(uint32_t)s * 1e-10;
+            af.y = 0.5;
+            af.r2 = 0.5;
+        } else {
+            af = polar_draws(s, s3f);
+        }
+        const bool nearf = defer && livef && !(g.debug_flags & 1) && glibc_log_near1(af.r2);
         const uint64_t nmf = __ballot(nearf);
         if (nmf) {
             if (nearf) {
@@ -796,8 +803,8 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
             top += __popcll(nmf);
         }
         if (!nearf && livef) {
-            const double lg = defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
-            const double mult = sqrt(-2 * lg / af.r2);
+            const double lg = (g.debug_flags & 1) ? 0.0 : defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
+            const double mult = (g.debug_flags & 1) ? af.r2 : sqrt(-2 * lg / af.r2);
             const double xm = af.x * mult;
             const double ym = af.y * mult;
             store_pair(g, p0, p1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);

@@ -767,11 +767,29 @@ __device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q
 // One needed 64-rank chunk c of the dense generation: lane l holds rank 64 c + l, whose attempt starts at
 // state s (any value for ranks past the call's end). di: the chunk's index in the host list (chunk_dest).
 // Near-1 lanes go on the wave's LDS stack (top: its uniform height), batches of 64 are finished here.
-__device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long long A, long long c, int di, uint64_t s,
-                                            int lane, bool defer, Near1Slot *stk, int &top,
+// The fast-chunk descriptor of list entry di (arr -1: the general path).
+__device__ __forceinline__ ChunkDest chunk_dest_of(const RngGeom &g, uint64_t f, int di)
+{
+    return g.chunk_dest[f] && !g.debug_flags ? g.chunk_dest[f][di] : ChunkDest{0, 0, 0, -1, 0, 0};
+}
+
+// Lane k's descriptor (held one per lane, K3r) as a uniform value: four v_readlane, no memory access.
+__device__ __forceinline__ ChunkDest chunk_dest_lane(const ChunkDest &mine, int k)
+{
+    static_assert(sizeof(ChunkDest) == 16, "ChunkDest is read as four dwords");
+    int w[4];
+    __builtin_memcpy(w, &mine, 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = __builtin_amdgcn_readlane(w[i], k);
+    ChunkDest cd;
+    __builtin_memcpy(&cd, w, 16);
+    return cd;
+}
+
+__device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long long A, long long c, const ChunkDest cd,
+                                            uint64_t s, int lane, bool defer, Near1Slot *stk, int &top,
                                             RngStateDev *__restrict__ sout)
 {
-    const ChunkDest cd = g.chunk_dest[f] ? g.chunk_dest[f][di] : ChunkDest{0, 0, 0, -1, 0, 0};
     if (cd.arr >= 0) { // uniform
         // fast chunk (host-built ChunkDest): no lane is past the call or its last attempt, the stored positions
         // are one run [lo, hi) in one stream array with at most one row wrap - no stream position search
@@ -783,16 +801,9 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
         double *const p0 = e0 >= cd.lo && e0 < cd.hi ? base + e0 + (e0 >= cd.wr ? cd.jump : 0) : nullptr;
         double *const p1 = e1 >= cd.lo && e1 < cd.hi ? base + e1 + (e1 >= cd.wr ? cd.jump : 0) : nullptr;
         const bool livef = p0 || p1;
-        uint64_t s3f = s;
-        PolarAttempt af{};
-        if (g.debug_flags & 4) { // timing ablations only, as the general path below
-            af.x = (double)(uint32_t)s * 1e-10;
-            af.y = 0.5;
-            af.r2 = 0.5;
-        } else {
-            af = polar_draws(s, s3f);
-        }
-        const bool nearf = defer && livef && !(g.debug_flags & 1) && glibc_log_near1(af.r2);
+        uint64_t s3f;
+        const PolarAttempt af = polar_draws(s, s3f);
+        const bool nearf = defer && livef && glibc_log_near1(af.r2);
         const uint64_t nmf = __ballot(nearf);
         if (nmf) {
             if (nearf) {
@@ -803,8 +814,8 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
             top += __popcll(nmf);
         }
         if (!nearf && livef) {
-            const double lg = (g.debug_flags & 1) ? 0.0 : defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
-            const double mult = (g.debug_flags & 1) ? af.r2 : sqrt(-2 * lg / af.r2);
+            const double lg = defer ? glibc_log_main(af.r2) : polar_log(g, af.r2);
+            const double mult = sqrt(-2 * lg / af.r2);
             const double xm = af.x * mult;
             const double ym = af.y * mult;
             store_pair(g, p0, p1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
@@ -910,7 +921,7 @@ __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_ke
         // the next chunk's states are in flight while this chunk computes
         const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
         const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
-        dense_chunk(g, f, A, c, i0 + k, s, lane, defer, stk, top, sout);
+        dense_chunk(g, f, A, c, chunk_dest_of(g, f, i0 + k), s, lane, defer, stk, top, sout);
         c = cn;
         s = sn;
     }
@@ -1059,6 +1070,8 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
     const long long c0 = uniform((int)pc.c0), cend = c0 + uniform((int)pc.n);
     long long G, grand;
     int skip;
+    // the piece's (<= 12) chunk descriptors, one per lane, loaded once beside the locate
+    const ChunkDest cds = lane < (int)pc.n ? chunk_dest_of(g, f, (int)pc.li0 + lane) : ChunkDest{0, 0, 0, -1, 0, 0};
     const bool found = locate_rank(g, c0 * 64, lane, G, skip, grand);
     if (p == g.npieces[f] - 1 && lane == 0 && grand < A) *err = 1; // not enough attempts launched: host re-sizes
     if (!found) return;
@@ -1116,7 +1129,7 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
         while (c < cend && R >= min((c + 1) * 64, A)) { // every rank of chunk c is in the ring
             const uint64_t rs = ring[(c * 64 + lane) & 127];
             const uint64_t s = RECOUNT ? (rs - kPcgInc) * kPcgMultInv : rs;
-            dense_chunk(g, f, A, c, (int)pc.li0 + (int)(c - c0), s, lane, defer, stk, top, sout);
+            dense_chunk(g, f, A, c, chunk_dest_lane(cds, (int)(c - c0)), s, lane, defer, stk, top, sout);
             ++c;
         }
         __asm__ volatile("" ::: "memory");

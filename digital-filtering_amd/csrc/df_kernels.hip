@@ -1078,6 +1078,7 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
     G = uniform((int)G);
     long long R = c0 * 64 - uniform(skip); // rank of group G's first accepted attempt
     const long long r_lo = c0 * 64, r_end = min(cend * 64, A);
+    const int span = (int)(r_end - r_lo);
     // lane's attempt 64 G + lane: its start state s0 (RECOUNT: s1, 1 step on, and s3, 3 steps on, instead)
     uint64_t st, s3 = 0;
     {
@@ -1110,9 +1111,9 @@ __global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kern
             acc = (mw >> (G & 15)) & 1u;
         }
         const uint64_t m = __ballot(acc);
-        const long long rank = R + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (acc && rank >= r_lo && rank < r_end) ring[rank & 127] = st;
+        const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        // rank R + below, compared in 32 bits against the piece's span (R - r_lo is uniform, the span <= 768)
+        if (acc && (unsigned)((int)(R - r_lo) + below) < (unsigned)span) ring[((int)R + below) & 127] = st;
         R += __popcll(m);
         ++G;
         if (RECOUNT) {

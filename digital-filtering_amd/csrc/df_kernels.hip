@@ -983,19 +983,26 @@ __global__ __launch_bounds__(1024) void rng_share_scan_kernel(RngGeom g, const i
 __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &G, int &skip, long long &grand)
 {
     const int W = g.xworld;
-    long long tot = 0;
-    for (int s = lane; s < W; s += 64) tot += *reinterpret_cast<const long long *>(g.xbuf + (size_t)s * g.xstride + g.xtot_off);
-    long long incl = tot; // shares in lane order (W <= 64: checked at create)
+    int s = 0;
+    long long Tl = T;
+    if (W == 1) { // one share (one GPU): its total only bounds T, so the block search below need not wait for it
+        grand = *reinterpret_cast<const long long *>(g.xbuf + g.xtot_off);
+    } else {
+        long long tot = 0;
+        for (int sh = lane; sh < W; sh += 64)
+            tot += *reinterpret_cast<const long long *>(g.xbuf + (size_t)sh * g.xstride + g.xtot_off);
+        long long incl = tot; // shares in lane order (W <= 64: checked at create)
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long y = __shfl_up(incl, o);
+            if (lane >= o) incl += y;
+        }
+        grand = __shfl(incl, 63);
+        if (T >= grand) return false;
+        const uint64_t ms = __ballot(lane < W && T < incl && T >= incl - tot);
+        s = __builtin_ctzll(ms);
+        Tl = T - __shfl(incl - tot, s);
     }
-    grand = __shfl(incl, 63);
-    if (T >= grand) return false;
-    const uint64_t ms = __ballot(lane < W && T < incl && T >= incl - tot);
-    const int s = __builtin_ctzll(ms);
-    const long long Tl = T - __shfl(incl - tot, s);
     const uint8_t *rec = g.xbuf + (size_t)s * g.xstride;
     const int *lp = reinterpret_cast<const int *>(rec + g.xlp_off);
     const int n = g.xchunk;
@@ -1019,7 +1026,7 @@ __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &
         b = lo + last;
         break;
     }
-    if (b < 0) return false;
+    if (b < 0 || T >= grand) return false;
     const long long Tb = Tl - __shfl(lp[min(lo + lane, n - 1)], b - lo);
     const int cnt = rec[(size_t)b * 64 + lane];
     int gin = cnt;

@@ -982,19 +982,10 @@ __global__ __launch_bounds__(1024) void rng_share_scan_kernel(RngGeom g, const i
 // counts -> the group.
 __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &G, int &skip, long long &grand)
 {
-    constexpr double kPerBlock = 3216.990877275948; // 4096 * pi / 4 accepts per block
-    const int W = g.xworld, n = g.xchunk;
-    // The share is guessed from equal expected totals and the first 64-block window of its prefixes is loaded
-    // before the exact share is known, so that load does not wait for the shares' totals (a wrong guess, near
-    // a share boundary, reloads); the window's values are kept for the block's own prefix below.
-    const double per = (double)n * kPerBlock;
-    const int sg = W == 1 ? 0 : min(W - 1, max(0, (int)((double)T / per)));
-    int lo = max(0, min((int)(((double)T - sg * per) * (1.0 / kPerBlock)) - 32, n - 64));
-    const int *lpg = reinterpret_cast<const int *>(g.xbuf + (size_t)sg * g.xstride + g.xlp_off);
-    int v = lo + lane < n ? lpg[lo + lane] : 0x7fffffff;
-    int s = sg;
+    const int W = g.xworld;
+    int s = 0;
     long long Tl = T;
-    if (W == 1) { // one share (one GPU): its total only bounds T
+    if (W == 1) { // one share (one GPU): its total only bounds T, so the block search below need not wait for it
         grand = *reinterpret_cast<const long long *>(g.xbuf + g.xtot_off);
     } else {
         long long tot = 0;
@@ -1011,35 +1002,32 @@ __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &
         const uint64_t ms = __ballot(lane < W && T < incl && T >= incl - tot);
         s = __builtin_ctzll(ms);
         Tl = T - __shfl(incl - tot, s);
-        if (s != sg) { // the guess missed the share: its window, from the exact share-local rank
-            lo = max(0, min((int)((double)Tl * (1.0 / kPerBlock)) - 32, n - 64));
-            const int *lps = reinterpret_cast<const int *>(g.xbuf + (size_t)s * g.xstride + g.xlp_off);
-            v = lo + lane < n ? lps[lo + lane] : 0x7fffffff;
-        }
     }
     const uint8_t *rec = g.xbuf + (size_t)s * g.xstride;
     const int *lp = reinterpret_cast<const int *>(rec + g.xlp_off);
+    const int n = g.xchunk;
+    int lo = (int)((double)Tl * (1.0 / 3216.990877275948)) - 32; // 4096 * pi / 4 accepts per block
+    lo = max(0, min(lo, n - 64));
     int b = -1;
     for (int it = 0; it < 1 << 16; ++it) { // bounded: each step moves the window towards T
-        const bool le = lo + lane < n && (long long)v <= Tl; // lp is nondecreasing
+        const int i = lo + lane;
+        const bool le = i < n && (long long)lp[i] <= Tl; // lp is nondecreasing
         const uint64_t m = __ballot(le);
         if (m == 0) {
             if (lo == 0) break; // cannot happen (lp[0] = 0 <= Tl)
             lo = max(0, lo - 63);
-            v = lo + lane < n ? lp[lo + lane] : 0x7fffffff;
             continue;
         }
         const int last = 63 - __builtin_clzll(m);
         if (last == 63 && lo + 64 < n) {
             lo += 63;
-            v = lo + lane < n ? lp[lo + lane] : 0x7fffffff;
             continue;
         }
         b = lo + last;
         break;
     }
     if (b < 0 || T >= grand) return false;
-    const long long Tb = Tl - __shfl(v, b - lo);
+    const long long Tb = Tl - __shfl(lp[min(lo + lane, n - 1)], b - lo);
     const int cnt = rec[(size_t)b * 64 + lane];
     int gin = cnt;
 #pragma unroll

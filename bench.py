@@ -216,6 +216,20 @@ def self_launch(argv, n, cmd=None, timeout_s=None):
     timer.daemon = True
     timer.start()
     line_out = None
+    interrupted = None
+
+    class Interrupted(Exception):
+        pass
+
+    # the ranks run in their own session, so a SIGTERM / SIGINT / SIGHUP meant for this launcher
+    # (an outer `timeout`, Ctrl-C, a closed terminal) would not reach them. Turn it into an exception here so
+    # the finally block below ends their process group before this process exits.
+    def on_signal(signum, frame):
+        raise Interrupted(signum)
+
+    handled = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
+    previous = {sig: signal.signal(sig, on_signal) for sig in handled}
+    rc = 1
     try:
         for line in proc.stdout:
             st = line.strip()
@@ -226,9 +240,28 @@ def self_launch(argv, n, cmd=None, timeout_s=None):
                 sys.stderr.write(line)
                 sys.stderr.flush()
         rc = proc.wait()
+    except Interrupted as e:
+        interrupted = e.args[0]
+        progress(f"signal {interrupted} received: terminating the ranks")
     finally:
         timer.cancel()
-    if expired.is_set():
+        for sig in handled:  # no second handler run while the group is being ended
+            signal.signal(sig, signal.SIG_IGN)
+        if proc.poll() is None:
+            for sig, wait in ((signal.SIGTERM, 10.0), (signal.SIGKILL, 5.0)):
+                try:
+                    os.killpg(proc.pid, sig)
+                    proc.wait(wait)
+                    break
+                except ProcessLookupError:
+                    break
+                except subprocess.TimeoutExpired:
+                    pass
+        for sig, h in previous.items():
+            signal.signal(sig, h)
+    if interrupted is not None:
+        rc = 128 + int(interrupted)
+    elif expired.is_set():
         rc = 124
     elif rc == 0 and line_out is None:
         progress("the launched ranks exited 0 without a JSON line")

@@ -201,7 +201,10 @@ struct df_handle {
     int nsets = 2;
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
-    int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds)
+    int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
+    int yt_rows = 4;         // ypass_t64: rows per wave (1, 2, 4, 8)
+    int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
+    int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
     RngGeom geom{};
     // halo
@@ -359,6 +362,11 @@ SweepArgs sweep_args(df_handle *h)
     }
     a.ydepth = h->ydepth;
     a.ylds = h->ylds;
+    a.ylist = h->ylist;
+    a.ylist_n = h->ylist_n;
+    a.ylist_nrb = h->ylist_nrb;
+    a.ylist_ncol = h->ylist_ncol;
+    a.ylist_R = h->yt_rows;
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -1006,6 +1014,36 @@ int upload_ycoop2_perm(df_handle *h, int c)
     return upload(h, h->c[c].ycoop2_perm, h->ycoop2_perm_host[c].data(), h->ycoop2_perm_host[c].size());
 }
 
+// Dispatch order of ypass_t64_kernel (ylds 3): blocks of 4 * yt_rows rows x 64 columns of every component, the
+// largest union of noise rows (a block's chunk count, so its time) first; ties keep component, tile, row order.
+int build_ylist(df_handle *h)
+{
+    const int Ny = h->Ny, RB = 4 * h->yt_rows;
+    const int ncol = (h->Nz_loc + 63) / 64, nrb = (Ny + RB - 1) / RB;
+    const int n = 3 * ncol * nrb;
+    if (n > h->ylist_cap) return fail(DF_EINVAL, "ypass_t64 tile list larger than its allocation");
+    std::vector<std::pair<int, int>> cost(n); // (-noise rows, tile)
+    for (int c = 0; c < 3; ++c)
+        for (int ct = 0; ct < ncol; ++ct)
+            for (int rb = 0; rb < nrb; ++rb) {
+                const int *nst = h->y_nst[c].data() + (size_t)(ct >> 1) * Ny;
+                int lo = 1 << 30, hi = -(1 << 30);
+                for (int j = rb * RB; j < std::min(Ny, rb * RB + RB); ++j) {
+                    lo = std::min(lo, j - nst[j]);
+                    hi = std::max(hi, j + nst[j]);
+                }
+                const int t = (c * ncol + ct) * nrb + rb;
+                cost[t] = {-(hi - lo + 1), t};
+            }
+    std::stable_sort(cost.begin(), cost.end(), [](const auto &p, const auto &q) { return p.first < q.first; });
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = cost[i].second;
+    h->ylist_n = n;
+    h->ylist_nrb = nrb;
+    h->ylist_ncol = ncol;
+    return upload(h, h->ylist, order.data(), order.size());
+}
+
 // This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
 int plan_strips(df_handle *h)
 {
@@ -1314,6 +1352,11 @@ int alloc_components(df_handle *h)
         if ((rc = dalloc_t(h, &d.Nz_st, Nst[1].size()))) return rc;
         if ((rc = upload(h, d.Ny_st, Nst[0].data(), Nst[0].size()))) return rc;
         if ((rc = upload(h, d.Nz_st, Nst[1].data(), Nst[1].size()))) return rc;
+        if (c == 2 && h->coeff_mode == DF_COEFF_TABLE && !s.per_cell) { // ypass_t64's list, sized for 1 row per wave
+            h->ylist_cap = 3 * ((h->Nz_loc + 63) / 64) * ((Ny + 3) / 4);
+            if ((rc = dalloc_t(h, &h->ylist, h->ylist_cap))) return rc;
+            if ((rc = build_ylist(h))) return rc;
+        }
         if (s.per_cell) {
             std::vector<int> nc[2];
             for (int dir = 0; dir < 2; ++dir) {
@@ -1398,7 +1441,9 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         record_layout(h->rng_blocks, &st1, &lo, &to);
         record_layout(h->rng_chunk, &stw, &lo, &to);
         if ((rc = dalloc_t(h, &h->xbuf, (size_t)std::max(st1, stw * h->world)))) return rc;
-        if (h->world > 64) return fail(DF_EINVAL, "more than 64 z-strip ranks"); // run generation's share lookup
+        // the run generation's share lookup holds at most 64 shares: split counting with it needs <= 64 ranks
+        if (h->world > 64 && h->gen_dense == 2 && !h->rng_replicate)
+            return fail(DF_EINVAL, "more than 64 z-strip ranks with split counting (set rng_replicate 1)");
     }
     h->geom.nb_groups = (long long)h->rng_blocks * 64;
     if ((rc = dalloc_t(h, &h->tasks, (size_t)nb_pad * kWavesPerBlock))) return rc;
@@ -1684,10 +1729,14 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
     h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
-    // z-strip handles in table mode (split counting, the fused exchange): generations two calls ahead
-    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE) h->look = 2;
+    // z-strip handles in table mode, one process per GPU (split counting, the fused exchange): generations two
+    // calls ahead. look is consulted only by fused_active() handles (one generation per hand-off), so in-process
+    // groups and batched handles keep look 1 and the noise sets their batch needs (a batched handle
+    // with look 2 was cut to 4 sets where its epochs need 2 * hb).
+    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->look = 2;
     if (const char *e = std::getenv("DFAMD_LOOKAHEAD")) h->look = std::atoi(e) >= 2 ? 2 : 1;
-    if (h->look == 2) h->nsets = 4;
+    if (h->hb > 1) h->look = 1;
+    if (h->look == 2) h->nsets = std::max(h->nsets, 4);
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -2238,7 +2287,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"zunroll", h->zunroll},
         {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ydepth", h->ydepth},
-        {"ylds", h->ylds}, {"handoff_batch", h->hb_conf},
+        {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"handoff_batch", h->hb_conf},
         {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"fused_exchange", h->fused_x}, {"k3a_fast", h->k3a_fast}};
     for (const auto &kv : keys)
         if (k == kv.first) {
@@ -2280,9 +2329,17 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         }
     }
     else if (k == "k3a_fast") h->k3a_fast = value != 0;
-    else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on
+    else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
     else if (k == "ydepth") h->ydepth = value < 0 ? 0 : value > 2 ? 2 : value;
-    else if (k == "ylds") h->ylds = value ? 2 : 0; // LDS-staged table y-pass (2: two chunks in flight; 0: off)
+    else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
+        if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
+        h->ylds = value == 3 ? 3 : value ? 2 : 0;
+    } else if (k == "yt_rows") {
+        if (value != 1 && value != 2 && value != 4 && value != 8) return fail(DF_EINVAL, "yt_rows must be 1, 2, 4 or 8");
+        h->yt_rows = value;
+        if (h->ylist)
+            if (int rc = build_ylist(h)) return rc;
+    }
     else if (k == "halo_overlap") {
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
@@ -2308,6 +2365,8 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     }
     else if (k == "rng_replicate") { // collective form changes: set it alike on every rank before the first df_filter
         if (h->group) return fail(DF_EINVAL, "rng_replicate applies to RCCL or single handles, not in-process groups");
+        if (!value && h->world > 64 && h->gen_dense == 2)
+            return fail(DF_EINVAL, "the run generation's share lookup holds at most 64 split-counting ranks");
         h->rng_replicate = value != 0;
         h->split_count = (h->comm || h->solo_strip) && !h->rng_replicate;
     }
@@ -2335,12 +2394,14 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             if ((rc = restart_pipeline(h, value))) return rc;
         } else h->hb = value;
     }
-    else if (k == "gen_dense") {
+    else if (k == "gen_dense") { // collective form changes on split-counting handles: the same on every rank
+        if (value < 0 || value > 2) return fail(DF_EINVAL, "gen_dense must be 0, 1 (Kc + K3a) or 2 (run generation)");
+        if (value == 2 && h->world > 64 && h->split_count)
+            return fail(DF_EINVAL, "the run generation's share lookup holds at most 64 split-counting ranks");
         if (value && h->device >= 0 && !h->geom.cstate) {
             int rc = alloc_dense(h);
             if (rc) return rc;
         }
-        if (value < 0 || value > 2) return fail(DF_EINVAL, "gen_dense must be 0, 1 (Kc + K3a) or 2 (run generation)");
         h->gen_dense = value;
     }
     else if (k == "fast_log") {

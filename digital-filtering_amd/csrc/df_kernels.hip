@@ -2212,9 +2212,137 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
     }
 }
 
+// K4 table mode, long chains, round 5 (SweepArgs::ylds 3): the LDS-staged block of ypass_tlds_kernel cut finer
+// for planes whose y-pass is a few hundred thousand cells of chains up to ~425 taps (the reference's own grid:
+// 510 x 400, N_y 14-212). One cell per lane, so a block covers a 64-column tile (the grid's 400 columns are 7
+// tiles with one 16-column tail instead of 4 strips with a 16-column tail that idled a quarter of the waves),
+// and R rows per wave, so each noise value read from LDS serves R products (R = 1 made the LDS array, not the
+// FP64 pipe, the limit). Blocks run in the host's order (SweepArgs::ylist): heaviest union of noise rows
+// first, components and tiles interleaved, so the widest stencils (N_y 206-212 around j = 160-200) start
+// first instead of wherever their rows fall. Each row adds its taps in the order i = -N..N (noise rows
+// ascending) with df.cpp:373-375's products: bit-identical to every other form.
+template <int R, int NW, int C, int PD>
+__global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
+{
+    constexpr int LW = C / NW; // chunk rows each wave loads
+    static_assert(C % NW == 0, "chunk rows split evenly over the waves");
+    __shared__ double nbuf[2][C][64];
+    const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
+    const int tile = a.ylist[blockIdx.x];
+    const int nrb = a.ylist_nrb, ncol = a.ylist_ncol;
+    const int rb = tile % nrb, ct = (tile / nrb) % ncol, c = tile / (nrb * ncol);
+    if (!((a.comps_mask >> c) & 1)) return; // block-uniform
+    const int Ny = a.Ny, RB = NW * R, j0 = rb * RB;
+    const int *nst = a.Ny_st[c] + (size_t)(ct >> 1) * Ny; // tap ranges of the 128-cell strip holding the tile
+    int mlo = 1 << 30, mhi = -(1 << 30);                    // the block's noise rows
+    for (int q = 0; q < RB && j0 + q < Ny; ++q) {
+        const int N = nst[j0 + q];
+        mlo = min(mlo, j0 + q - N);
+        mhi = max(mhi, j0 + q + N);
+    }
+    const int jw = j0 + w * R;
+    int lo[R], hi[R];
+    const double *tb[R]; // row r's full tap vector: tap t = m - lo[r] at tb[r][t]
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        lo[r] = 1 << 30;
+        hi[r] = -(1 << 30);
+        tb[r] = a.tabf;
+        if (jw + r < Ny) {
+            const int N = nst[jw + r];
+            lo[r] = jw + r - N;
+            hi[r] = jw + r + N;
+            tb[r] = a.tabf + a.tabf_off[N];
+        }
+    }
+    const int col = ct * 64 + lane; // < Pz: a padding column is loaded and summed but never stored
+    const double *np = a.ry[c] + (size_t)a.Nyp[c] * a.Pz + col; // noise row m at np + m * Pz
+    double pre[PD][LW];
+    auto gload = [&](auto K, int u0) {
+        constexpr int k0 = decltype(K)::value;
+#pragma unroll
+        for (int k = 0; k < LW; ++k) {
+            const int m = u0 + w + NW * k; // wave-uniform
+            pre[k0][k] = m <= mhi ? np[(ptrdiff_t)m * a.Pz] : 0.0;
+        }
+    };
+    auto lstore = [&](auto K, int buf) {
+        constexpr int k0 = decltype(K)::value;
+#pragma unroll
+        for (int k = 0; k < LW; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
+    };
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0;
+    auto compute = [&](int u0, int buf) {
+        const int mb = min(u0 + C - 1, mhi);
+        bool full = mb == u0 + C - 1, any = false;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            full = full && lo[r] <= u0 && hi[r] >= mb;
+            any = any || (lo[r] <= mb && hi[r] >= u0);
+        }
+        if (full) { // every row of the wave takes all C noise rows of the chunk
+            const double *cb[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) cb[r] = tb[r] + (u0 - lo[r]);
+#pragma unroll
+            for (int q = 0; q < C; ++q) {
+                const double n = nbuf[buf][q][lane];
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] += cb[r][q] * n;
+            }
+        } else if (any) {
+            for (int m = u0; m <= mb; ++m) {
+                const double n = nbuf[buf][m - u0][lane];
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (m >= lo[r] && m <= hi[r]) acc[r] += tb[r][m - lo[r]] * n; // wave-uniform
+            }
+        }
+    };
+    // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
+    // ypass_tlds_kernel)
+    const int nch = (mhi - mlo) / C + 1;
+    gload(ic_t<0>{}, mlo);
+    if constexpr (PD > 1) gload(ic_t<1 % PD>{}, mlo + C);
+    lstore(ic_t<0>{}, 0);
+    __syncthreads();
+    auto step = [&](auto K, int i) {
+        constexpr int k = decltype(K)::value;
+        if (i + PD < nch) gload(K, mlo + (i + PD) * C); // block-uniform
+        compute(mlo + i * C, i & 1);
+        if (i + 1 < nch) lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+        __syncthreads();
+    };
+    for (int i = 0; i < nch; i += PD) {
+        step(ic_t<0>{}, i);
+        if constexpr (PD > 1)
+            if (i + 1 < nch) step(ic_t<1 % PD>{}, i + 1);
+    }
+    if (col >= a.Nz_loc) return;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (jw + r >= Ny) continue;
+        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.Nzp[c] + col;
+        if (a.ynt_stores) __builtin_nontemporal_store(acc[r], o);
+        else *o = acc[r];
+    }
+}
+
 template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
 {
     if constexpr (TABLE) {
+        if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
+            const dim3 grid((unsigned)a.ylist_n);
+            switch (a.ylist_R) {
+            case 1: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 2: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 8: hipLaunchKernelGGL((ypass_t64_kernel<8, 4, 16, 1>), grid, dim3(256), 0, st, a); break;
+            default: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            }
+            return hipGetLastError();
+        }
         if (a.ylds && !a.per_cell) {
             const int nrowblk = (a.Ny + 4 * R - 1) / (4 * R);
             const unsigned blocks = (unsigned)(((long long)a.nstrips * nrowblk + 7) / 8 * 8);

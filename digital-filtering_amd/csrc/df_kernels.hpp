@@ -150,6 +150,10 @@ struct SweepArgs {
     const int *ycoop2_perm[3]; // dispatch position -> tile inside each run (nullptr: ascending)
     int ydepth;                // table y-pass: 1 ypass_table_kernel (2: 3 noise groups ahead at 4 rows); 0 the shared kernel
     int ylds;                  // table y-pass with the noise staged in LDS per block of 4R rows (ypass_tlds_kernel)
+    // ylds 3 (ypass_t64_kernel): blocks of 4 ylist_R rows x 64 columns, launched in the order ylist[0, ylist_n)
+    // (tile = (c * ylist_ncol + column tile) * ylist_nrb + row block; heaviest union of noise rows first)
+    const int *ylist;
+    int ylist_n, ylist_nrb, ylist_ncol, ylist_R;
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

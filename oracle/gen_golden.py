@@ -89,8 +89,13 @@ def native_fixture(seed=42, dt=1e-8, nsteps=2, sample_rows=(1, 100, 300, 509)):
     json.dump(meta, open(os.path.join(OUT, f"native_s{seed}.json"), "w"), indent=1)
 
 
+def sha256(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
+
+
 def synth_fixture(name, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, dt2=None, nsteps2=0, full_steps=(),
-                  sample_rows=None, csv_head=0):
+                  sample_rows=None, csv_head=0, hashes=False):
     with tempfile.TemporaryDirectory() as d:
         extra = [dt2, nsteps2] if nsteps2 else []
         run("synth", RUN_ROOT, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, d, *extra)
@@ -117,6 +122,8 @@ def synth_fixture(name, seed, Ny, Nz, Nmin, Nmax, dt, nsteps, dt2=None, nsteps2=
             arr[f"s{s}_{k}_rows"] = stp[k][list(sample_rows)]
             if s in full_steps:
                 arr[f"s{s}_{k}"] = stp[k]
+            if hashes:  # the whole field, bit for bit, in 64 hex digits (planes too large to keep)
+                arr[f"s{s}_{k}_sha256"] = np.array(sha256(stp[k]))
     np.savez_compressed(os.path.join(OUT, f"{name}.npz"), **arr)
     json.dump(meta, open(os.path.join(OUT, f"{name}.json"), "w"), indent=1)
 
@@ -209,7 +216,8 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     if len(sys.argv) > 1:  # regenerate named fixtures only, e.g. `gen_golden.py writers`
         for name in sys.argv[1:]:
-            {"writers": lambda: writers_fixture("writers_native_s42")}[name]()
+            {"writers": lambda: writers_fixture("writers_native_s42"), "c2": c2_fixture}[name]()
+        manifest()
         return
     kat()
     rng_fixture(42)
@@ -228,6 +236,17 @@ def main():
     rms_fixture("rms_native_s42", 42)
     # the reference's file writers on its native grid: per-call CSV, write_tecplot, plot_RST_lerp
     writers_fixture("writers_native_s42")
+    c2_fixture()
+    manifest()
+
+
+def c2_fixture():
+    # c2 (BASELINE configs[1]): 512 x 512, N 4-32 by the SURVEY 8d rule, step 0 + 2 x filter(1e-8): sampled rows,
+    # stats and the sha256 of every whole field at every step (round 5)
+    synth_fixture("c2_s42", 42, 512, 512, 4, 32, 1e-8, 2, sample_rows=(0, 1, 100, 128, 256, 511), hashes=True)
+
+
+def manifest():
     manifest = {
         "generator": "oracle/gen_golden.py",
         "reference": "connorswitala/digital-filtering @ /root/reference (df.cpp compiled unmodified, "
@@ -237,6 +256,7 @@ def main():
     }
     json.dump(manifest, open(os.path.join(OUT, "MANIFEST.json"), "w"), indent=1)
     print("wrote", OUT)
+    return manifest
 
 
 if __name__ == "__main__":

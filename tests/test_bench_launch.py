@@ -95,3 +95,34 @@ def test_bare_bench_ranks_record_their_phases(tmp_path):
     for rank in (0, 1):
         lines = (tmp_path / f"rank{rank}.log").read_text().splitlines()
         assert lines and lines[-1].endswith("dry-run"), lines
+
+
+def test_signal_to_the_launcher_ends_the_ranks(tmp_path):
+    # the ranks run in their own session; a SIGTERM to the launcher (an outer `timeout`) must end
+    # their process group too, not leave them holding the GPUs
+    import signal
+    import time
+    pidf = tmp_path / "child.pid"
+    child = f"import os, time; open({str(pidf)!r}, 'w').write(str(os.getpid())); time.sleep(120)"
+    launcher = (f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+                f"sys.exit(bench.self_launch([], 2, cmd=[sys.executable, '-c', {child!r}], timeout_s=600))")
+    p = subprocess.Popen([sys.executable, "-c", launcher], env=_env(), stderr=subprocess.PIPE, text=True)
+    t0 = time.monotonic()
+    while not pidf.exists() or not pidf.read_text():
+        assert time.monotonic() - t0 < 60 and p.poll() is None
+        time.sleep(0.1)
+    cpid = int(pidf.read_text())
+    p.send_signal(signal.SIGTERM)
+    rc = p.wait(60)
+    err = p.stderr.read()
+    assert rc == 128 + signal.SIGTERM, (rc, err[-2000:])
+    assert "terminating the ranks" in err
+    for _ in range(100):  # the child is gone (reaped by the launcher before it exited)
+        try:
+            os.kill(cpid, 0)
+        except ProcessLookupError:
+            break
+        time.sleep(0.1)
+    else:
+        os.kill(cpid, signal.SIGKILL)
+        raise AssertionError("the rank outlived its launcher")

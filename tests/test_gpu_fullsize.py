@@ -360,3 +360,38 @@ def test_multi_gpu_planes_whole_bitexact_vs_oracle(tmp_path, name, Ny, Nz):
     spec = dict(plane="synthetic", seed=78, device=0, Ny=Ny, Nz=Nz, N_min=4, N_max=64)
     check_against_oracle([dfamd.DigitalFilter(coeff_mode="table", **spec)], ref, name + " table")
     check_against_oracle(dfamd.create_group(8, coeff_mode="packed", **spec), ref, name + " packed x8 strips")
+
+
+def test_c3_whole_plane_bitexact_vs_reference(tmp_path):
+    """c3 (BASELINE configs[2]) against the REFERENCE ITSELF, not the restatement: the
+    reference's df.cpp, compiled here by oracle/ref/Makefile into oracle/_ref/ref_harness (the binary bench.py's
+    cpu_baseline already runs on this box), builds the 2048 x 2048 N 4-64 plane with its own setup code, runs
+    step 0 and one filter(1e-8) and dumps its fields; both coefficient modes must equal them bit for bit. The
+    harness is part of the snapshot whenever the reference was built, so a missing binary fails here."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "oracle", "_ref", "ref_harness")
+    run_root = os.path.join(root, "oracle", "_ref", "run_root")
+    assert os.path.exists(exe) and os.path.isdir(run_root), "oracle/_ref not built (make -C oracle/ref)"
+    seed = 42
+    r = subprocess.run([exe, "synth", run_root, str(seed), "2048", "2048", "4", "64", "1e-8", "1", str(tmp_path)],
+                       capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    n = 2048 * 2048
+    ref = {(s, k): np.fromfile(str(tmp_path / f"step{s}_{k}.bin")).reshape(2048, 2048)
+           for s in (0, 1) for k in ("u", "v", "w", "T", "rho")}
+    assert all(a.size == n for a in ref.values())
+    nys = np.fromfile(str(tmp_path / "Nys_u.bin"), dtype=np.int32).reshape(2048, 2048)
+    # the reference's own half-widths follow the SURVEY 8d rule this plane is named by
+    assert np.array_equal(nys[:, 0], [O.synthetic_N(j, 2048, 4, 64) for j in range(2048)])
+    rng = O.Rng(seed=seed)
+    O.Filter(rng=rng)  # the harness runs the reference's native constructor first on the same static stream
+    for mode in ("table", "packed"):
+        h = dfamd.DigitalFilter(plane="synthetic", device=0, coeff_mode=mode, resume=rng.state, **C3)
+        for s in (0, 1):
+            if s:
+                h.filter(1e-8)
+            for k in ("u", "v", "w", "T", "rho"):
+                assert np.array_equal(h.field(k), ref[(s, k)]), (mode, s, k)
+        h.close()

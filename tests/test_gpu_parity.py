@@ -143,12 +143,26 @@ def check_golden_case(name, coeff_mode="packed", rows_per_wave=8):
             assert_stats(a, g[f"s{s}_{k}_stats"], (name, s, k))
             if s in full:
                 assert_same(a, g[f"s{s}_{k}"], f"{name} step {s} {k}")
+            if f"s{s}_{k}_sha256" in g:  # the whole field bit for bit against the reference's own output
+                assert field_sha256(a) == str(g[f"s{s}_{k}_sha256"]), (name, s, k)
     return f
+
+
+def field_sha256(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
 
 
 @pytest.mark.parametrize("name", ["c1_s42", "ramp256_s1234", "ragged_s7"])
 def test_golden_synthetic(name):
     check_golden_case(name)
+
+
+@pytest.mark.parametrize("mode", ["packed", "table"])
+def test_golden_c2_bitexact_vs_reference(mode):
+    # c2 (BASELINE configs[1], 512 x 512, N 4-32) against the reference's own output (tests/golden/c2_s42.npz,
+    # oracle/gen_golden.py: df.cpp compiled here): every whole field at step 0 and after two calls, by sha256
+    check_golden_case("c2_s42", coeff_mode=mode, rows_per_wave=0)
 
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8, ycoop=0)),
@@ -176,6 +190,8 @@ def test_golden_native_grid(mode, tuning):
                                          ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1)),
                                          ("table", dict(ylds=1)), ("table", dict(ylds=2, rows_per_wave=2)),
                                          ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
+                                         ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
+                                         ("table", dict(ylds=3, yt_rows=8)),
                                          ("table", dict(ylds=0, ydepth=0))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
@@ -308,6 +324,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
                 dict(ylds=1, rows_per_wave=8), dict(ylds=0)]
+    if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back
+        settings += [dict(ylds=3, yt_rows=1), dict(yt_rows=2), dict(yt_rows=8), dict(yt_rows=4), dict(ylds=2), dict(ylds=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

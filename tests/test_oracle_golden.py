@@ -77,6 +77,13 @@ def _check_case(f, g, steps_dt):
             assert np.array_equal(a[rows], g[f"s{s}_{k}_rows"]), (s, k)
             if s in full:
                 assert np.array_equal(a, g[f"s{s}_{k}"]), (s, k)
+            if f"s{s}_{k}_sha256" in g:  # the whole field against the reference's (planes too large to keep)
+                assert field_sha256(a) == str(g[f"s{s}_{k}_sha256"]), (s, k)
+
+
+def field_sha256(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
 
 
 def test_native_grid_bitexact(golden):
@@ -93,7 +100,7 @@ def test_native_grid_bitexact(golden):
     _check_case(f, g, [float(g["dt"])] * int(g["nsteps"]))
 
 
-@pytest.mark.parametrize("name", ["c1_s42", "ramp256_s1234", "ragged_s7"])
+@pytest.mark.parametrize("name", ["c1_s42", "ramp256_s1234", "ragged_s7", "c2_s42"])
 def test_synthetic_planes_bitexact(golden, name):
     g = golden(f"{name}.npz")
     rng = O.Rng(seed=int(g["seed"]))

@@ -37,7 +37,7 @@ for step in "$@"; do
     bench) timeout -k 10 900 python3 bench.py $arg > "$base.json" 2> "$base.log"; rc=$?
            [ $rc -eq 0 ] && python3 tools/bench_summary.py "$base.json" ;;
     bench8emu) start=$(date +%s)
-           DFAMD_EMULATE_HOSTS=1 timeout -k 10 900 python3 bench.py --gpus 8 $arg > "$base.json" 2> "$base.log"; rc=$?
+           DFAMD_EMULATE_HOSTS=1 DFAMD_BENCH_TIMEOUT=870 timeout -k 10 900 python3 bench.py --gpus 8 $arg > "$base.json" 2> "$base.log"; rc=$?
            echo "wall_s $(( $(date +%s) - start ))" | tee "$base.wall"
            [ $rc -eq 0 ] && python3 tools/bench_summary.py "$base.json" ;;
     strip) timeout -k 10 400 python3 tools/strip_timing.py $arg > "$base.json" 2> "$base.log"; rc=$?; cat "$base.json" ;;

@@ -113,21 +113,15 @@ struct df_handle {
     // table z-pass noise staged in LDS; 2 (default): 16-B copies, every load issued before the LDS stores
     // (c3 table z-pass 0.142 -> 0.129 ms, call -2.5%; profiles/r2/ab_zstage2_zquad_table.jsonl)
     int zstage = 2;
-    int ablate_handoff = 0; // DFAMD_ABLATE_HANDOFF: timing-only ablation of the per-call stream hand-off
     int fuse_plan = 0; // small planes: K3 plans its own waves, no K2/K2c launch (RngGeom::fused_plan)
     // Dense generation (RngGeom::gen_dense: compaction through memory, one wave per needed 64-rank chunk,
     // near-1 log lanes deferred). Default in table mode (VALU-bound, where K3's skeleton costs); packed
     // keeps the compacted K3 (its RNG hides under the HBM-bound sweeps; the dense form adds 2 x 8 B per
     // stored pair of traffic). Never on planes that use fused_plan or gen_split > 1 (small planes).
     int gen_dense = 0;
-    int ywindow = 1;   // table y-pass coefficient windows on uniform-N tiles
-    // table y-pass: noise and coefficients loaded a whole 4-tap group ahead (ypass_kernel): c3 y-pass
-    // 0.141 -> 0.133 ms alone, the reference's grid and c2 -4.5% per call (profiles/r2/ab_ydeep_table.jsonl)
-    int ydeep = 1;
     int ycoop = 0;     // packed y-pass, block-cooperative tiles (set for long tap chains in plan_strips)
     int zsplit = 0;    // packed z-pass, a wave per component (set for planes with few tiles in plan_strips)
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
-    int ydepth = 1;      // table y-pass, 1-2 rows per wave: 16 noise rows in flight (SweepArgs::ydepth)
     int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
                          // consecutive tiles, heaviest group first (balance_ycoop2)
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
@@ -205,7 +199,7 @@ struct df_handle {
     int yt_rows = 4;         // ypass_t64: rows per wave (1, 2, 4, 8)
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
-    int k3a_fast = 1; // K3a takes host-built destinations for chunks that land in one r_ys array (ChunkDest)
+    bool dense_ready = false; // the run generation's chunk tables are built (alloc_dense)
     RngGeom geom{};
     // halo
     double *send_l = nullptr, *send_r = nullptr, *recv_l = nullptr, *recv_r = nullptr;
@@ -347,8 +341,6 @@ SweepArgs sweep_args(df_handle *h)
     a.rowc = h->rowc;
     a.comps_mask = 7;
     a.yunroll = h->yunroll;
-    a.ywindow = h->ywindow;
-    a.ydeep = h->ydeep;
     a.ycoop = h->ycoop;
     a.ycoop2_run = 0;
     for (int c = 0; c < 3; ++c)
@@ -360,7 +352,6 @@ SweepArgs sweep_args(df_handle *h)
         a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
         a.ycoop2_perm[c] = h->ycoop_order ? h->c[c].ycoop2_perm : nullptr;
     }
-    a.ydepth = h->ydepth;
     a.ylds = h->ylds;
     a.ylist = h->ylist;
     a.ylist_n = h->ylist_n;
@@ -488,14 +479,14 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     const int set = gen_set(h, gi);
     rs = h->overlap ? h->rng_stream : h->stream;
     // the epoch's sets were last read by epoch e - 2 (2*hb sets), released when epoch e - 1 began
-    if (gen_pos(h, gi) == 0 && (h->hb == 1 || e >= 2) && !(h->ablate_handoff & 2))
+    if (gen_pos(h, gi) == 0 && (h->hb == 1 || e >= 2))
         HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e & 1], 0), DF_EHIP);
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
-    g.gen_dense = h->gen_dense && h->geom.cstate && !g.fused_plan && g.gen_split == 1 ? h->gen_dense : 0;
+    g.gen_dense = h->gen_dense == 2 && h->dense_ready && !g.fused_plan && g.gen_split == 1 ? 2 : 0;
     if (g.gen_dense == 2) { // K1 writes the group counts of its share's record, K2s the share's prefix
         g.xbuf = h->xbuf;
         g.xworld = h->split_count ? h->world : 1;
@@ -504,7 +495,6 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     } else {
         g.xbuf = nullptr;
     }
-    if (!h->k3a_fast) g.chunk_dest[0] = g.chunk_dest[1] = nullptr;
     for (int c = 0; c < 3; ++c) {
         g.ry[c] = h->c[c].ry[set];
         g.rz[c] = h->c[c].rz[set];
@@ -633,13 +623,12 @@ int consume_gen(df_handle *h)
     const long long gi = h->gen_used, e = gen_epoch(h, gi);
     const bool first = gen_pos(h, gi) == 0;
     int rc;
-    // DFAMD_ABLATE_HANDOFF (timing only, wrong results possible): 1 no wait for the noise, 2 no release
-    if (first && gi > (h->hb == 1 ? 0 : h->gen_base) && !(h->ablate_handoff & 2))
+    if (first && gi > (h->hb == 1 ? 0 : h->gen_base))
         HIP_OR(hipEventRecord(h->ev_release[(e - 1) & 1], h->stream), DF_EHIP); // the previous epoch's sets free
     const long long need = h->hb == 1 ? gi + 1 : h->gen_base + (e + 1) * h->hb; // this epoch, launched
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
-    if (first && !(h->ablate_handoff & 1)) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[e & 1], 0), DF_EHIP);
+    if (first) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[e & 1], 0), DF_EHIP);
     h->cur = gen_set(h, gi);
     h->gen_used++;
     return DF_OK;
@@ -669,7 +658,7 @@ int prefetch_gen(df_handle *h)
 bool fused_active(const df_handle *h)
 {
     return h->fused_x && h->split_count && h->world > 1 && (h->comm || h->solo_strip) && !h->group && h->overlap &&
-           h->hb == 1 && h->gen_dense == 2 && h->geom.cstate;
+           h->hb == 1 && h->gen_dense == 2 && h->dense_ready;
 }
 
 // Start of a visible step: the next generation's K1 (its group counts) on rng_stream, ev_counted after it.
@@ -931,9 +920,9 @@ int read_config(df_handle *h, const df_config_c *cfg)
     h->world = cfg->world < 1 ? 1 : cfg->world;
     if (h->rank < 0 || h->rank >= h->world) return fail(DF_EINVAL, "rank out of range");
     h->rows_per_wave = cfg->rows_per_wave; // 0: chosen from the plane's shape after setup (below)
-    // tuning knobs for in-process A/B experiments (tools/ab.py); defaults are the measured best
-    if (const char *e = std::getenv("DFAMD_YUNROLL")) h->yunroll = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_ZUNROLL")) h->zunroll = std::atoi(e);
+    // Timing-only environment: DFAMD_RNG_OVERLAP=0 runs the noise on the sweep stream
+    // (profilers), DFAMD_SOLO_STRIP one rank of a split plane alone, DFAMD_SOLO_XCHG_US its exchange held,
+    // DFAMD_RNG_DEBUG the RNG ablations (wrong results by design). Launch shapes are df_set_tuning keys.
     if (const char *e = std::getenv("DFAMD_RNG_OVERLAP")) h->overlap = std::atoi(e);
     if (const char *e = std::getenv("DFAMD_SOLO_STRIP")) h->solo_strip = std::atoi(e) && cfg->world > 1 && !cfg->comm_id;
     if (const char *e = std::getenv("DFAMD_SOLO_XCHG_US")) h->solo_xchg_us = h->solo_strip ? std::atof(e) : 0;
@@ -943,7 +932,6 @@ int read_config(df_handle *h, const df_config_c *cfg)
     // its sweeps are HBM-bound and hide the replicated count (equal within noise at N = 4, 8;
     // profiles/r2/strip_timing_c4_counts_only.jsonl).
     h->rng_replicate = h->coeff_mode == DF_COEFF_PACKED ? 1 : 0;
-    if (const char *e = std::getenv("DFAMD_RNG_REPLICATE")) h->rng_replicate = std::atoi(e) != 0;
     if (h->solo_strip && !h->rng_replicate) h->split_count = true;
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
     if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
@@ -1074,12 +1062,12 @@ int plan_strips(df_handle *h)
         if (h->coeff_mode == DF_COEFF_TABLE) h->rows_per_wave = long_chain ? 1 : 4;
         else if (long_chain || tiny) {
             h->rows_per_wave = 1;
-            if (!std::getenv("DFAMD_YUNROLL")) h->yunroll = 8;
+            h->yunroll = 8;
         } else h->rows_per_wave = 2;
         // table mode, long chains: the noise staged in LDS per block of 4 rows, 2 chunks in flight (ylds): the
         // reference's grid y-pass 0.051 -> 0.043 ms, call -9%; c3 and c2 (short chains, FP64-issue-bound) lose
         // with it (profiles/r3/bd)
-        if (h->coeff_mode == DF_COEFF_TABLE && long_chain && !std::getenv("DFAMD_YLDS")) h->ylds = 2;
+        if (h->coeff_mode == DF_COEFF_TABLE && long_chain) h->ylds = 2;
         // Long chains, packed: one block per row pair, noise loads shared by both rows, the next chunk in
         // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
         // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
@@ -1101,19 +1089,12 @@ int plan_strips(df_handle *h)
     // ab_fuse_plan_packed.jsonl). Packed planes with long y chains keep
     // the scan-and-plan launch: the fused K3's extra waves beside the row-pair y-pass cost the
     // reference's grid 11% (profiles/r2/ab_fuse_plan.jsonl).
-    if (const char *e = std::getenv("DFAMD_ZSPLIT")) h->zsplit = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_YCOOP")) h->ycoop = std::atoi(e);
     h->fuse_plan = h->coeff_mode == DF_COEFF_TABLE || h->ycoop < 7 ? 1 : 0;
-    if (const char *e = std::getenv("DFAMD_FUSE_PLAN")) h->fuse_plan = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_ABLATE_HANDOFF")) h->ablate_handoff = std::atoi(e);
     // Table mode generates its noise through the run form (round 4: group counts, one wave per piece of needed
     // chunks): with split counting it needs no pass over the whole stream after the exchange and its counts
     // travel in the halo group (c4 over 8, one rank: 0.25-0.26 -> 0.24 ms per call, profiles/r4/d); on one GPU
     // it is even with Kc + K3a (c3 0.364 vs 0.366 ms, profiles/r4/e).
     h->gen_dense = h->coeff_mode == DF_COEFF_TABLE ? 2 : 0;
-    if (const char *e = std::getenv("DFAMD_GEN_DENSE")) h->gen_dense = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_YLDS")) h->ylds = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_K3A_FAST")) h->k3a_fast = std::atoi(e);
     const int Ny = s.Ny;
     for (int c = 0; c < 3; ++c) {
         CompDev &d = h->c[c];
@@ -1145,7 +1126,7 @@ int plan_strips(df_handle *h)
             by += h->c[c].by_size;
             bz += h->c[c].bz_size;
         }
-        if (h->coeff_mode != DF_COEFF_TABLE && !std::getenv("DFAMD_NO_WRITE_WINDOWS")) {
+        if (h->coeff_mode != DF_COEFF_TABLE) {
             if (8 * by >= 2000000000LL) h->ywin_T = 4096, h->ywin_W = 256;
             if (8 * bz >= 2000000000LL) h->zwin_T = 4096, h->zwin_W = 256;
         }
@@ -1178,7 +1159,6 @@ int plan_rng(df_handle *h)
         g.inv_width[sidx] = (W == 1) ? 0 : (uint64_t)(~0ull / W) + 1;
     }
     g.fast_log = 2; // glibc's own log in the polar transform: normals bit-identical (tests/test_rng_log.py)
-    if (const char *e = std::getenv("DFAMD_FAST_LOG")) g.fast_log = std::atoi(e);
     g.nt_stores = 1; // noise written past the caches: it is read once, by the next call's sweeps (A/B -1.4%)
     const PcgJump next = pcg_jump(4ull * 64); // attempt start -> the lane's next attempt start
     g.next_mult = next.mult;
@@ -1206,7 +1186,6 @@ int plan_rng(df_handle *h)
     g.gen_split = 1;
     while (g.gen_split < kRngPerThread && (long long)h->rng_blocks * kWavesPerBlock * g.gen_split < 4096)
         g.gen_split *= 2;
-    if (const char *e = std::getenv("DFAMD_GEN_SPLIT")) g.gen_split = std::atoi(e);
     if (g.gen_split < 1 || g.gen_split > kRngPerThread || (g.gen_split & (g.gen_split - 1)))
         return fail(DF_EINVAL, "gen_split must be a power of two <= 16");
     return DF_OK;
@@ -1224,20 +1203,15 @@ int open_device(df_handle *h, int device)
     // the memory-bound sweeps keep their waves; the compute-bound RNG fills gaps.
     int prio_lo = 0, prio_hi = 0;
     HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
-    int use_prio = 0; // measured: priorities cost 1-2% wall time (in-process A/B, tools/ab.py)
-    if (const char *e = std::getenv("DFAMD_RNG_PRIO")) use_prio = std::atoi(e);
+    const int use_prio = 0; // measured: priorities cost 1-2% wall time (in-process A/B, tools/ab.py)
     HIP_OR(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, use_prio ? prio_hi : 0), DF_EHIP);
     HIP_OR(hipStreamCreateWithPriority(&h->rng_stream, hipStreamNonBlocking, use_prio ? prio_lo : 0), DF_EHIP);
     // The two streams' per-call hand-offs (noise ready, noise set free) order kernels on this GPU and
     // are never waited on by the host (df_sync synchronizes the streams themselves), so they are
     // recorded without the system-scope fence: the reference's grid -2.2%, c2 -1.5% (packed) /
     // -3.6% (table) per call, c3 unchanged (profiles/r2/ab_event_scope.jsonl; a device-scope
-    // release instead was neutral). DFAMD_EVENT_SCOPE=system|device restores either form.
-    unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
-    if (const char *e = std::getenv("DFAMD_EVENT_SCOPE")) {
-        if (std::string(e) == "system") ev_flags = hipEventDisableTiming;
-        else if (std::string(e) == "device") ev_flags = hipEventDisableTiming | hipEventReleaseToDevice;
-    }
+    // release instead was neutral).
+    const unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
     for (int set = 0; set < 2; ++set) {
         HIP_OR(hipEventCreateWithFlags(&h->ev_rng[set], ev_flags), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], ev_flags), DF_EHIP);
@@ -1314,9 +1288,7 @@ int alloc_components(df_handle *h)
     // of two boxes (profiles/r2/pool/; order By0 By1 By2 Bz0 Bz1 Bz2 = 2 gains a little less). Same
     // bytes, same kernels: where the 20 GB stream lands is all that changes (presumably larger physical
     // fragments for one large allocation, i.e. fewer address-translation misses; not measured).
-    // DFAMD_B_POOL=0 allocates them one by one.
-    int pool = 1;
-    if (const char *e = std::getenv("DFAMD_B_POOL")) pool = std::atoi(e);
+    const int pool = 1;
     const int Ny = s.Ny;
     int rc;
     const size_t n_loc = (size_t)Ny * h->Nz_loc;
@@ -1504,10 +1476,10 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
     return upload(h, h->rstate, &st0, 1);
 }
 
-// Dense generation tables (RngGeom::gen_dense): for each parity f of the incoming cached normal, the
+// Run generation tables (RngGeom::gen_dense 2): for each parity f of the incoming cached normal, the
 // 64-rank chunks whose pairs (positions f + 2r, f + 2r + 1) store something on this GPU - the same
 // columns as stream_dest: r_ys columns [z0, z1), r_zs pads on the plane's first/last strip - plus the
-// chunk of the call's last rank A - 1 (it sets the stream state). Bitmap for Kc, list for K3a.
+// chunk of the call's last rank A - 1 (it sets the stream state); their fast destinations and the pieces.
 int alloc_dense(df_handle *h)
 {
     const RngGeom &g = h->geom;
@@ -1516,7 +1488,7 @@ int alloc_dense(df_handle *h)
     if (nch >= (1ull << 31)) return fail(DF_EINVAL, "plane too large for the dense generation tables");
     std::vector<uint32_t> bits[2], list[2];
     for (int f = 0; f < 2; ++f) {
-        bits[f].assign((nch + 31) / 32 + 2, 0u); // + 2 padding words: Kc reads a 64-bit window
+        bits[f].assign((nch + 31) / 32 + 2, 0u); // host bitmap of the needed chunks, listed below
         const long long A = (long long)((g.Q - f + 1) / 2);
         auto mark = [&](uint64_t qa, uint64_t qb) { // positions [qa, qb)
             if (qb <= qa || qb < (uint64_t)f + 1) return;
@@ -1544,7 +1516,7 @@ int alloc_dense(df_handle *h)
         for (uint64_t c = 0; c < nch; ++c)
             if ((bits[f][c >> 5] >> (c & 31)) & 1u) list[f].push_back((uint32_t)c);
     }
-    // K3a / K3r fast chunks: no rank past the call or the call's last (that one sets the stream state), all 128
+    // K3r fast chunks: no rank past the call or the call's last (that one sets the stream state), all 128
     // positions in one stream array with at most one row wrap, and the positions this GPU stores (stream_dest:
     // r_ys columns [z0, z1), the r_zs pads of the plane's edge strips) one run [lo, hi) whose destinations are
     // affine in the position on either side of the wrap: destinations by arithmetic. Round 4: r_zs pads and
@@ -1570,8 +1542,6 @@ int alloc_dense(df_handle *h)
         return true;
     };
     std::vector<ChunkDest> dest[2];
-    bool fast_partial = true;
-    if (const char *e = std::getenv("DFAMD_FAST_PARTIAL")) fast_partial = std::atoi(e) != 0;
     for (int f = 0; f < 2; ++f) {
         const long long A = (long long)((g.Q - f + 1) / 2);
         dest[f].resize(std::max<size_t>(1, list[f].size()), ChunkDest{0, 0, 0, -1, 0, 0});
@@ -1611,7 +1581,6 @@ int alloc_dense(df_handle *h)
             }
             if (!ok || lo < 0 || wraps > 1) continue;
             if (hi < 0) hi = 128;
-            if (!fast_partial && (lo != 0 || hi != 128 || (su & 1))) continue; // timing A/B: round-3 rule only
             ChunkDest d{};
             d.off = d0;
             d.jump = (int)(d1 - d0);
@@ -1623,27 +1592,15 @@ int alloc_dense(df_handle *h)
         }
     }
     int rc;
-    uint32_t *db[2], *dl[2];
     for (int f = 0; f < 2; ++f) {
         ChunkDest *dd = nullptr;
         if ((rc = dalloc_t(h, &dd, dest[f].size()))) return rc;
         if ((rc = upload(h, dd, dest[f].data(), dest[f].size()))) return rc;
         h->geom.chunk_dest[f] = dd;
-        if ((rc = dalloc_t(h, &db[f], bits[f].size()))) return rc;
-        if ((rc = upload(h, db[f], bits[f].data(), bits[f].size()))) return rc;
-        if ((rc = dalloc_t(h, &dl[f], std::max<size_t>(1, list[f].size())))) return rc;
-        if (!list[f].empty() && (rc = upload(h, dl[f], list[f].data(), list[f].size()))) return rc;
-        h->geom.need_bits[f] = db[f];
-        h->geom.chunks[f] = dl[f];
-        h->geom.nchunks[f] = (int)list[f].size();
     }
-    uint64_t *cs = nullptr;
-    if ((rc = dalloc_t(h, &cs, nch * 64))) return rc;
-    h->geom.cstate = cs;
     // Run generation (gen_dense 2): the list cut into pieces of consecutive chunks, at most kRunPiece each and
     // of near-equal length within a run (a 9-chunk row segment of a strip is one piece, not 8 + 1)
-    uint32_t kRunPiece = 12;
-    if (const char *e = std::getenv("DFAMD_RUN_PIECE")) kRunPiece = (uint32_t)std::max(1, std::atoi(e));
+    const uint32_t kRunPiece = 12; // piece lengths 6 / 12 / 24 / 48 measured: 12 kept (profiles/r4/n)
     for (int f = 0; f < 2; ++f) {
         std::vector<RunPiece> pcs;
         const std::vector<uint32_t> &L = list[f];
@@ -1665,6 +1622,7 @@ int alloc_dense(df_handle *h)
         h->geom.pieces[f] = dp;
         h->geom.npieces[f] = (int)pcs.size();
     }
+    h->dense_ready = true;
     return DF_OK;
 }
 
@@ -1691,7 +1649,6 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_xchg, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
-        if (const char *e = std::getenv("DFAMD_HALO_OVERLAP")) h->halo_overlap = std::atoi(e);
     }
     return DF_OK;
 }
@@ -1724,7 +1681,6 @@ int build(df_handle *h, const df_config_c *cfg)
         // let it run a call further ahead (c3: 0.366 -> 0.352 ms per call median, profiles/r4/e).
         if (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb == 1) h->hb = 2;
     }
-    if (const char *e = std::getenv("DFAMD_HANDOFF_BATCH")) h->hb = std::atoi(e);
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
     h->hb_conf = h->hb;
@@ -1734,7 +1690,6 @@ int build(df_handle *h, const df_config_c *cfg)
     // groups and batched handles keep look 1 and the noise sets their batch needs (a batched handle
     // with look 2 was cut to 4 sets where its epochs need 2 * hb).
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->look = 2;
-    if (const char *e = std::getenv("DFAMD_LOOKAHEAD")) h->look = std::atoi(e) >= 2 ? 2 : 1;
     if (h->hb > 1) h->look = 1;
     if (h->look == 2) h->nsets = std::max(h->nsets, 4);
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
@@ -1745,7 +1700,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = upload_tables(h))) return rc;
     if ((rc = alloc_components(h))) return rc;
     if ((rc = alloc_rng(h, cfg))) return rc;
-    if (h->gen_dense && h->geom.gen_split == 1 && (rc = alloc_dense(h))) return rc;
+    if (h->gen_dense == 2 && h->geom.gen_split == 1 && (rc = alloc_dense(h))) return rc;
     if ((rc = open_comm(h, cfg))) return rc;
     for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
@@ -2285,10 +2240,12 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     if (!h || !key || !value) return fail(DF_EINVAL, "null handle, key or value");
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
-        {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"zunroll", h->zunroll},
-        {"ycoop", h->ycoop}, {"ycoop_order", h->ycoop_order}, {"ydepth", h->ydepth},
-        {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"handoff_batch", h->hb_conf},
-        {"halo_overlap", h->halo_overlap}, {"gen_dense", h->gen_dense}, {"fused_exchange", h->fused_x}, {"k3a_fast", h->k3a_fast}};
+        {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
+        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"zsplit", h->zsplit},
+        {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
+        {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
+        {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
+        {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap}};
     for (const auto &kv : keys)
         if (k == kv.first) {
             *value = kv.second;
@@ -2309,28 +2266,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->rows_per_wave = value;
     }
     else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
-    else if (k == "zunroll") h->zunroll = value >= 4 ? 4 : 2;
-    else if (k == "nt_stores") h->nt_stores = h->ynt_stores = value != 0;
-    else if (k == "znt_stores") h->nt_stores = value != 0;
-    else if (k == "ynt_stores") h->ynt_stores = value != 0;
-    else if (k == "zstage") h->zstage = value ? 2 : 0; // the element copy (1) is only the unaligned fallback now
-    else if (k == "ywindow") h->ywindow = value != 0; // shared y-pass kernel, table mode (ydepth 0)
-    else if (k == "ydeep") h->ydeep = value != 0;
+    else if (k == "nt_stores") h->nt_stores = h->ynt_stores = h->geom.nt_stores = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
-    else if (k == "ycoop_ovh") {
-        if (value < 0) return fail(DF_EINVAL, "ycoop_ovh must be >= 0");
-        h->ycoop_ovh = value;
-        if (valid_dev(h)) {
-            if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
-            for (int c = 0; c < 3; ++c) {
-                balance_ycoop2(h, c);
-                if (int rc = upload_ycoop2_perm(h, c)) return rc;
-            }
-        }
-    }
-    else if (k == "k3a_fast") h->k3a_fast = value != 0;
+    else if (k == "zstage") h->zstage = value ? 2 : 0; // 0: the unstaged table z-pass that large halos take (tests)
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
-    else if (k == "ydepth") h->ydepth = value < 0 ? 0 : value > 2 ? 2 : value;
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
@@ -2377,7 +2316,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value && !h->send_l && (rc = alloc_halo(h))) return rc;
         h->halo_loopback = value;
     }
-    else if (k == "rng_nt_stores") h->geom.nt_stores = value != 0;
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
@@ -2395,10 +2333,11 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         } else h->hb = value;
     }
     else if (k == "gen_dense") { // collective form changes on split-counting handles: the same on every rank
-        if (value < 0 || value > 2) return fail(DF_EINVAL, "gen_dense must be 0, 1 (Kc + K3a) or 2 (run generation)");
+        if (value != 0 && value != 2)
+            return fail(DF_EINVAL, "gen_dense must be 0 (compacted K3) or 2 (run generation)");
         if (value == 2 && h->world > 64 && h->split_count)
             return fail(DF_EINVAL, "the run generation's share lookup holds at most 64 split-counting ranks");
-        if (value && h->device >= 0 && !h->geom.cstate) {
+        if (value && h->device >= 0 && !h->dense_ready) {
             int rc = alloc_dense(h);
             if (rc) return rc;
         }

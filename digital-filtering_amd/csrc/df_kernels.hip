@@ -21,9 +21,6 @@ namespace dfamd {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// Timing-only ablations (Makefile `variant`): DF_ABLATE_NOISE replaces every noise load
-// of the sweeps by a register value, DF_ABLATE_COEF every coefficient load. Results are
-// wrong by design; the product is never built with either.
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(3))) dvec2 *lds_pair_ptr; // LDS-staged noise (ds_read_b128)
 __device__ __forceinline__ double2 ld_pair(const double2 *p) { return *p; }
@@ -32,24 +29,10 @@ __device__ __forceinline__ double2 ld_pair(lds_pair_ptr p)
     const dvec2 v = *p;
     return make_double2(v.x, v.y);
 }
-#if defined(DF_ABLATE_NOISE)
-#define DF_NOISE(ptr, tag) make_double2((double)(tag), (double)(threadIdx.x & 63))
-#else
-#define DF_NOISE(ptr, tag) ld_pair(ptr)
-#endif
-// DF_ABLATE_TCOEF: table-mode coefficients become an inline constant (no scalar loads).
-#if defined(DF_ABLATE_TCOEF)
-#define DF_TCOEF(x) 0.5
-#else
-#define DF_TCOEF(x) (x)
-#endif
 
 // Coefficient stream load: read once per call, so optionally non-temporal.
 template <bool NT> __device__ __forceinline__ double2 ldB(const double *p)
 {
-#if defined(DF_ABLATE_COEF)
-    return make_double2((double)(size_t)p, 1.0);
-#endif
     if (NT) {
         const dvec2 v = __builtin_nontemporal_load(reinterpret_cast<const dvec2 *>(p));
         return make_double2(v.x, v.y);
@@ -636,93 +619,19 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
     }
 }
 
-// ---------------------------------------------------------------- dense generation (gen_dense)
+// ---------------------------------------------------------------- chunk generation (run generation)
 //
 // The compacted K3 above spends more time in its per-wave skeleton (ring appends, batch loop, per-lane
 // destination walk, mostly scalar and branch work: 29M SALU against 37M VALU per c3 table call) than in
-// the transform. The dense form moves the compaction through memory instead:
-//   Kc  one wave per attempt wave: its first rank from the scan, its accept flags (K1's masks or the
-//       screen recomputed), and for each accepted attempt whose 64-rank chunk stores something here the
-//       attempt's start state into cstate[rank] (consecutive ranks: coalesced 8-B stores);
-//   K3a one wave per kDenseG needed chunks (host-built list for the call's parity f), lane l of chunk c =
-//       rank 64c + l: the state from cstate (the next chunk's loaded while this one computes), the four
-//       draws, the transform, the pair's destination by arithmetic (consecutive lanes, consecutive 16-B
-//       pairs). Every lane busy but the partial chunks at the pad edges; no skipped batches, no ring.
-//       glibc's near-1 band (6.25% of r2, so present in 98% of 64-lane batches) is not evaluated in the
-//       chunk's batch: those lanes push (x, y, destinations) on a wave-private LDS stack, popped 64 at a
-//       time into batches of their own (the near-1 half of glibc_log alone), the rest at the wave's end.
-// Same draws, same arithmetic (x*x + y*y and the log's band test recomputed bit for bit), same
-// destinations as K3: bit-identical noise.
-
-__global__ __launch_bounds__(kRngThreads) void rng_dense_compact_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                                       const long long *__restrict__ offsets,
-                                                                       const long long *__restrict__ part,
-                                                                       const int *__restrict__ wave_counts,
-                                                                       const uint16_t *__restrict__ masks,
-                                                                       int nb_total)
-{
-    constexpr int WPB = kRngThreads / 64;
-    const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
-    const int b = blockIdx.x, gw = b * WPB + w;
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    if (gw == 0 && lane == 0 && f) { // the normal cached by the previous call is stream position 0
-        double *d = stream_dest(g, stream_pos(g, 0));
-        if (d) *d = sin->saved * 1.0 + 0.0;
-    }
-    if (b >= nb_total) return;
-    // the block's offset and its four waves' counts, loaded together
-    const long long ob = offsets[b] + part[b >> 10];
-    const int4 wc = *reinterpret_cast<const int4 *>(wave_counts + (size_t)b * WPB);
-    const long long r_lo = ob + (w > 0 ? wc.x : 0) + (w > 1 ? wc.y : 0) + (w > 2 ? wc.z : 0);
-    const int nw = w == 0 ? wc.x : w == 1 ? wc.y : w == 2 ? wc.z : wc.w;
-    if (r_lo >= A || nw == 0) return;
-    const long long r_end = min(r_lo + (long long)nw, A); // this wave's ranks [r_lo, r_end)
-    // needed bits of the wave's chunks [c_lo, c_hi] (<= 17 of them): one 64-bit window of the bitmap
-    const long long c_lo = r_lo >> 6, c_hi = (r_end - 1) >> 6;
-    const uint32_t *nb = g.need_bits[f] + (c_lo >> 5); // the bitmap has two padding words
-    const uint64_t win = ((uint64_t)nb[0] | ((uint64_t)nb[1] << 32)) >> (c_lo & 31);
-    const int span = (int)(c_hi - c_lo); // < 32
-    const uint32_t need = (uint32_t)win & ((2u << span) - 1u);
-    if (!need) return;
-    const int tid = w * 64 + lane;
-    const uint32_t bits = g.recount ? lane_accept_bits(g, sin->state, b, tid) : masks[(size_t)b * kRngThreads + tid];
-    uint64_t st = thread_first_state(g, sin->state, b, tid);
-    long long R = r_lo; // uniform: rank of this iteration's first accepted attempt
-    if (need == ((2u << span) - 1u)) {
-        // every chunk of the wave's ranks is needed (one GPU: all but the r_zs interior's): no per-iteration
-        // chunk tests; the wave's accepted attempts hold exactly the ranks [r_lo, r_lo + nw)
-#pragma unroll 4
-        for (int m = 0; m < kRngPerThread; ++m) {
-            const bool acc = (bits >> m) & 1u;
-            const uint64_t mask = __ballot(acc);
-            const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-            const long long rank = R + below;
-            if (acc && rank < A) g.cstate[rank] = st;
-            R += __popcll(mask);
-            st = g.next_mult * st + g.next_plus;
-        }
-        return;
-    }
-#pragma unroll 4
-    for (int m = 0; m < kRngPerThread; ++m) {
-        const bool acc = (bits >> m) & 1u;
-        const uint64_t mask = __ballot(acc);
-        const int n = __popcll(mask);
-        if (n && R < r_end) {
-            const int k0 = (int)((R >> 6) - c_lo), k1 = (int)(((R + n - 1) >> 6) - c_lo); // <= 2 chunks
-            if ((need >> k0) & (0xFFFFFFFFu >> (31 - (k1 - k0)))) {
-                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-                const long long rank = R + below;
-                if (acc && rank < A && ((need >> ((rank >> 6) - c_lo)) & 1u)) g.cstate[rank] = st;
-            }
-        }
-        R += n;
-        st = g.next_mult * st + g.next_plus;
-    }
-}
+// the transform. The run generation (K3r below) generates by 64-rank chunks instead: lane l of chunk c holds
+// rank 64c + l, draws its attempt's four outputs, transforms and stores the pair at a destination computed
+// by arithmetic (consecutive lanes, consecutive 16-B pairs). glibc's near-1 band (6.25% of r2, so present in
+// 98% of 64-lane batches) is not evaluated in the chunk's batch: those lanes push (x, y, destinations) on a
+// wave-private LDS stack, popped 64 at a time into batches of their own (the near-1 half of glibc_log
+// alone), the rest at the wave's end. Same draws, same arithmetic (x*x + y*y and the log's band test
+// recomputed bit for bit), same destinations as K3: bit-identical noise. (Round 3's two-kernel form of it -
+// Kc compacting accepted states into memory, K3a one wave per 8 chunks - was removed in round 5: no plane
+// selected it once K3r existed.)
 
 __device__ __forceinline__ void store_pair(const RngGeom &g, double *d0, double *d1, double n0, double n1)
 {
@@ -758,11 +667,6 @@ __device__ __forceinline__ void near1_batch(const RngGeom &g, const Near1Slot *q
     store_pair(g, e.d0, e.d1, ym * 1.0 + 0.0, xm * 1.0 + 0.0);
 }
 
-#if defined(DF_K3A_WPE)
-#define DF_K3A_ATTR __attribute__((amdgpu_waves_per_eu(DF_K3A_WPE)))
-#else
-#define DF_K3A_ATTR
-#endif
 
 // One needed 64-rank chunk c of the dense generation: lane l holds rank 64 c + l, whose attempt starts at
 // state s (any value for ranks past the call's end). di: the chunk's index in the host list (chunk_dest).
@@ -897,43 +801,9 @@ __device__ __forceinline__ void dense_chunk(const RngGeom &g, uint64_t f, long l
     }
 }
 
-// K3a: kDenseG needed chunks per wave (8; 4-128 measured alike, profiles/r3/e)
-constexpr int kDenseChunks = 8;
-template <int kDenseG>
-__global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
-                                                                        RngStateDev *__restrict__ sout)
-{
-    __shared__ Near1Slot stack_all[kRngThreads / 64][128]; // < 64 carried + 64 pushed per chunk
-    const int lane = threadIdx.x & 63, wv = uniform(threadIdx.x >> 6);
-    Near1Slot *stk = stack_all[wv];
-    const uint64_t f = (uint64_t)sin->saved_flag;
-    const int nch = g.nchunks[f];
-    const int i0 = (blockIdx.x * (kRngThreads / 64) + wv) * kDenseG;
-    if (i0 >= nch) return;
-    const int ng = min(kDenseG, nch - i0);
-    const long long A = (long long)((g.Q - f + 1) / 2);
-    const uint32_t *lst = g.chunks[f] + i0;
-    const bool defer = g.fast_log == 2;
-    int top = 0; // uniform stack height
-    long long c = uniform((int)lst[0]);
-    uint64_t s = c * 64 + lane < A ? g.cstate[c * 64 + lane] : 0;
-    for (int k = 0; k < ng; ++k) {
-        // the next chunk's states are in flight while this chunk computes
-        const long long cn = k + 1 < ng ? (long long)uniform((int)lst[k + 1]) : c;
-        const uint64_t sn = (k + 1 < ng && cn * 64 + lane < A) ? g.cstate[cn * 64 + lane] : 0;
-        dense_chunk(g, f, A, c, chunk_dest_of(g, f, i0 + k), s, lane, defer, stk, top, sout);
-        c = cn;
-        s = sn;
-    }
-    if (top > 0) {
-        __asm__ volatile("" ::: "memory");
-        near1_batch(g, stk, top, top, lane);
-    }
-}
-
 // ---------------------------------------------------------------- run generation (gen_dense 2)
 //
-// The dense form above needs every accepted attempt's state in cstate (Kc): with split counting Kc recomputes
+// Round 3's dense form needed every accepted attempt's state in memory: with split counting it recomputed
 // the accept flags of every attempt wave that feeds a needed chunk (a whole wave of 1024 attempts for a few
 // chunks: 40 us of a c4/8 table rank, profiles/r3/bl) behind a chain of scan kernels. The run form counts per
 // 64-attempt group instead (K1, one ballot each; the split-counting exchange carries these bytes), scans them
@@ -941,8 +811,8 @@ __global__ __launch_bounds__(kRngThreads) DF_K3A_ATTR void rng_dense_generate_ke
 // before the piece's first rank). One wave per piece (K3r) then walks the groups from there: each lane tests
 // its attempt of the group (K1's mask on one GPU, the same float screen under split counting), accepted lanes
 // of the piece append their state to a wave-private 128-slot LDS ring in rank order, and each completed chunk
-// goes through dense_chunk (the same draws, transform and destinations as K3a: bit-identical noise). A piece
-// of n chunks walks ~1.27 n + 1 groups; no cstate round trip, no per-wave pass over the whole stream.
+// goes through dense_chunk (the chunk generation above: bit-identical noise). A piece of n chunks walks
+// ~1.27 n + 1 groups; no round trip of states through memory, no per-wave pass over the whole stream.
 
 // K2s: one share's block prefix. One 1024-thread block over the share's xchunk block counts (K1's per-block
 // totals): the exclusive prefix of each block within the share (int32) and the share's total (int64), written
@@ -1043,18 +913,13 @@ __device__ bool locate_rank(const RngGeom &g, long long T, int lane, long long &
     return true;
 }
 
-#if defined(DF_K3R_WPE)
-#define DF_K3R_ATTR __attribute__((amdgpu_waves_per_eu(DF_K3R_WPE)))
-#else
-#define DF_K3R_ATTR
-#endif
 // K3r: one wave per piece (see above). RECOUNT (split counting): each lane screens its attempt of the group as
 // K1 does; the walk keeps the states one and three steps into the attempt (s1, s3: one multiply-add each per
 // group), the ring holds s1, and s0 = one step back when the chunk is generated. Otherwise (one GPU) the flags
 // are K1's masks: the 16 groups of one (block, wave) share a 16-bit word per lane (word (G >> 4) * 64 + lane,
 // bit G & 15), loaded once and the next one ahead; the walk keeps s0 alone.
 template <bool RECOUNT>
-__global__ __launch_bounds__(kRngThreads) DF_K3R_ATTR void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
+__global__ __launch_bounds__(kRngThreads) void rng_run_generate_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                       RngStateDev *__restrict__ sout,
                                                                       const uint16_t *__restrict__ masks,
                                                                       int *__restrict__ err)
@@ -1253,11 +1118,6 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
                              WaveTask *tasks, int *ntasks, int *err, int nb_total, int nb_scan, hipStream_t st)
 {
     const int nparts = (nb_scan + 1023) / 1024; // <= 1024: checked at create
-#if defined(DF_NO_SMALL_SCAN)
-    constexpr bool small_ok = false; // timing-only variant: always the three-kernel form
-#else
-    constexpr bool small_ok = true;
-#endif
     if (g.gen_dense == 2) { // run generation: K3r alone (K2s ran with K1, before any exchange)
         const int np = g.npieces[0] > g.npieces[1] ? g.npieces[0] : g.npieces[1];
         if (g.recount)
@@ -1268,25 +1128,9 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
                                st_out, masks, err);
         return hipGetLastError();
     }
-    if (g.gen_dense) {
-        if (small_ok && nb_scan <= 1024 && nb_total <= 1024)
-            hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
-                               wave_counts, nb_scan, 0, tasks, ntasks, err); // scan only (no plan: nb_total 0)
-        else {
-            hipLaunchKernelGGL(rng_scan_local_kernel, dim3(nparts), dim3(256), 0, st, counts, offsets, part, nb_scan);
-            hipLaunchKernelGGL(rng_scan_parts_kernel, dim3(1), dim3(1024), 0, st, part, nparts, st_in, g.Q, err, ntasks);
-        }
-        hipLaunchKernelGGL(rng_dense_compact_kernel, dim3(nb_total), dim3(kRngThreads), 0, st, g, st_in, offsets, part,
-                           wave_counts, masks, nb_total);
-        const int nch = g.nchunks[0] > g.nchunks[1] ? g.nchunks[0] : g.nchunks[1];
-        const int per_block = kDenseChunks * (kRngThreads / 64);
-        const dim3 grid((nch + per_block - 1) / per_block);
-        hipLaunchKernelGGL(rng_dense_generate_kernel<kDenseChunks>, grid, dim3(kRngThreads), 0, st, g, st_in, st_out);
-        return hipGetLastError();
-    }
     if (g.fused_plan) {
         // the compacted K3 plans its own waves (small planes: one launch fewer per call)
-    } else if (small_ok && nb_scan <= 1024 && nb_total <= 1024) {
+    } else if (nb_scan <= 1024 && nb_total <= 1024) {
         hipLaunchKernelGGL(rng_scan_plan_small_kernel, dim3(1), dim3(1024), 0, st, g, st_in, counts, offsets, part,
                            wave_counts, nb_scan, nb_total, tasks, ntasks, err);
     } else {
@@ -1326,13 +1170,8 @@ __device__ __forceinline__ void write_window(int T, int W)
 // i = -N..N. The coefficient stream is the only HBM-bound load: one 1 KiB
 // coalesced dwordx4 per (row, tap).
 
-#if defined(DF_YPASS_WPE)
-#define DF_YPASS_ATTR __attribute__((amdgpu_waves_per_eu(DF_YPASS_WPE)))
-#else
-#define DF_YPASS_ATTR
-#endif
 template <int R, bool TABLE, bool NT, int YU, bool PC>
-__global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, int nrowblk)
+__global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 {
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
@@ -1390,16 +1229,16 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
         if (TABLE) {
             const int i = t - r;
             if (!PC) {
-                const double b = DF_TCOEF(tb[r][i]);
+                const double b = tb[r][i];
                 return make_double2(b, b);
             }
             const int ai = i < 0 ? -i : i;
-            return make_double2(DF_TCOEF(tb[r][ai]), DF_TCOEF(tb1[r][ai]));
+            return make_double2(tb[r][ai], tb1[r][ai]);
         }
         return ldB<NT>(bp[r] + (ptrdiff_t)t * kStrip);
     };
     auto predicated = [&](int t) {
-        const double2 n = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t);
+        const double2 n = ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz));
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int i = t - r;
@@ -1410,19 +1249,9 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
             }
         }
     };
-    auto noise = [&](int t) { return DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t); };
-    auto body_n = [&](int t, const double2 n) {
-        double2 b[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) b[r] = coef(r, t);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            acc0[r] += b[r].x * n.x;
-            acc1[r] += b[r].y * n.y;
-        }
-    };
+    auto noise = [&](int t) { return ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz)); };
     auto body = [&](int t) {
-        const double2 n = DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t);
+        const double2 n = ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz));
         double2 b[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) b[r] = coef(r, t);
@@ -1439,11 +1268,6 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
     const int bh = body_ok ? Nlo : thi;
     int t = tlo;
     for (; t < bl; ++t) predicated(t);
-#if defined(DF_YPASS_NOPREFETCH)
-    constexpr bool kPrefetch = false; // timing-only variant
-#else
-    constexpr bool kPrefetch = true;
-#endif
     if (YU >= 8 && !PC && t + YU - 1 <= bh) {
         // Deep pipeline (yunroll 8): a ring of YU taps' noise and coefficients in registers;
         // slot u is refilled with tap t+u+YU right after it is consumed, so YU taps are always
@@ -1476,251 +1300,6 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
         for (int u = 0; u < YU; ++u) use(nb[u], cb[u]);
         t += YU;
     }
-    if constexpr (TABLE && !PC && YU < 4 && R <= 4) {
-        // Long chains (table mode takes 1-2 rows per wave where N_y >= 128, the reference's grid: up to 426
-        // taps per wave at ~3 waves per SIMD): the wave's serial chain of noise-row loads sets the time, so
-        // the noise runs kYD groups of 4 rows ahead in a register ring (16 rows in flight instead of 4-8);
-        // the group's coefficient window is a scalar load one group ahead. Same products, same order.
-        // 4 rows per wave (c3-class planes): 2 groups ahead, 105 VGPRs as before; c3 -0.8% per call, c2 +-1%
-        // (profiles/r3/bk)
-        constexpr int kYD = R <= 2 ? 4 : 2;
-        constexpr int WN = (R + 3 + 7) / 8 * 8;
-        if (a.ydeep && a.ywindow && a.ydepth && Nlo == Nhi && t + 4 * kYD - 1 <= bh) {
-            const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
-            double2 nq[kYD][4];
-            const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
-            const double *nl = np + (ptrdiff_t)t * Pz; // next group to load
-            auto ldn = [&](double2 (&nn)[4]) {
-                nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nl), 0);
-                nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P1), 1);
-                nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P2), 2);
-                nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P3), 3);
-                nl += P4;
-            };
-            auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                    for (int r = 0; r < R; ++r) {
-                        const double b = ww[u - r + R - 1];
-                        acc0[r] += b * nn[u].x;
-                        acc1[r] += b * nn[u].y;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            };
-            const double *wq = cb + t;
-            double w[WN];
-#pragma unroll
-            for (int k = 0; k < WN; ++k) w[k] = DF_TCOEF(wq[k]);
-#pragma unroll
-            for (int g = 0; g < kYD; ++g) ldn(nq[g]);
-            for (; t + 8 * kYD - 1 <= bh; t += 4 * kYD) { // the groups issued below stay within bh
-#pragma unroll
-                for (int g = 0; g < kYD; ++g) {
-                    double wn[WN];
-#pragma unroll
-                    for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]); // the table is padded past its last vector
-                    __builtin_amdgcn_sched_barrier(0);
-                    taps(nq[g], w);
-                    ldn(nq[g]); // group t + 4 (g + kYD)
-                    __builtin_amdgcn_sched_barrier(0);
-                    wq += 4;
-#pragma unroll
-                    for (int k = 0; k < WN; ++k) w[k] = wn[k];
-                }
-            }
-#pragma unroll
-            for (int g = 0; g < kYD; ++g) { // drain: groups t .. t + 4 kYD - 1, loaded, within bh
-                double wn[WN];
-#pragma unroll
-                for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]);
-                taps(nq[g], w);
-                wq += 4;
-#pragma unroll
-                for (int k = 0; k < WN; ++k) w[k] = wn[k];
-            }
-            t += 4 * kYD;
-        }
-    }
-    if (TABLE && !PC && YU < 4 && a.ydeep && a.ywindow && Nlo == Nhi && t + 7 <= bh) {
-        // The same deep pipeline on a tile whose R rows share one N (row-uniform planes, every tile but
-        // where N steps): tap t of row r uses b[t - r] of ONE vector, so a group's 4 taps x R rows need
-        // the R + 3 coefficients b[t - R + 1 .. t + 3], one scalar window (s_load_dwordx16 at R = 4)
-        // instead of R row loads and their address arithmetic. Same products, same order: bit-identical.
-        constexpr int WN = (R + 3 + 7) / 8 * 8;
-        const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
-        double2 nA[4], nB[4];
-        double wA[WN], wB[WN];
-        // running pointers (noise row t0, window of t0), advanced by a group per load: no per-group multiplies
-        const double *nq = np + (ptrdiff_t)t * Pz, *wq = cb + t;
-        const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
-        auto ld = [&](int, double2 (&nn)[4], double (&ww)[WN]) {
-            nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nq), 0);
-            nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P1), 1);
-            nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P2), 2);
-            nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nq + P3), 3);
-#pragma unroll
-            for (int k = 0; k < WN; ++k) ww[k] = DF_TCOEF(wq[k]); // the table is padded past its last vector
-            nq += P4;
-            wq += 4;
-        };
-        auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const double b = ww[u - r + R - 1];
-                    acc0[r] += b * nn[u].x;
-                    acc1[r] += b * nn[u].y;
-                }
-                // one tap's products at a time: the scheduler would otherwise compute a whole group's
-                // products first (123 -> 105 VGPRs; c3 table call -2%, profiles/r3/aa)
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
-        ld(t, nA, wA);
-        for (; t + 11 <= bh; t += 8) {
-            ld(t + 4, nB, wB);
-            __builtin_amdgcn_sched_barrier(0);
-            taps(nA, wA);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(t + 8, nA, wA);
-            __builtin_amdgcn_sched_barrier(0);
-            taps(nB, wB);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (t + 7 <= bh) {
-            ld(t + 4, nB, wB);
-            taps(nA, wA);
-            taps(nB, wB);
-            t += 8;
-        } else {
-            taps(nA, wA);
-            t += 4;
-        }
-    }
-    if (TABLE && !PC && YU < 4 && a.ydeep && t + 7 <= bh) {
-        // Table mode, deep pipeline (SweepArgs::ydeep): taps go in groups of 4 noise rows; the next
-        // group's noise (4 x 16 B per lane) and coefficients (R x 4 scalars) are loaded a whole group
-        // ahead, so every load has a full group of taps (16 R mul/add pairs) between issue and use.
-        // Same products, same order: bit-identical.
-        double2 nA[4], nB[4];
-        double cA[R][4], cB[R][4];
-        auto ld = [&](int t0, double2 (&nn)[4], double (&cc)[R][4]) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) nn[u] = noise(t0 + u);
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) cc[r][u] = DF_TCOEF(tb[r][t0 + u - r]);
-        };
-        auto taps = [&](const double2 (&nn)[4], const double (&cc)[R][4]) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    acc0[r] += cc[r][u] * nn[u].x;
-                    acc1[r] += cc[r][u] * nn[u].y;
-                }
-                __builtin_amdgcn_sched_barrier(0); // as above
-            }
-        };
-        ld(t, nA, cA);
-        for (; t + 11 <= bh; t += 8) {
-            // sched_barrier: keep the compiler from sinking the next group's loads into the taps
-            ld(t + 4, nB, cB);
-            __builtin_amdgcn_sched_barrier(0);
-            taps(nA, cA);
-            __builtin_amdgcn_sched_barrier(0);
-            ld(t + 8, nA, cA);
-            __builtin_amdgcn_sched_barrier(0);
-            taps(nB, cB);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (t + 7 <= bh) { // one more full group pair: A holds t..t+3
-            ld(t + 4, nB, cB);
-            taps(nA, cA);
-            taps(nB, cB);
-            t += 8;
-        } else {
-            taps(nA, cA);
-            t += 4;
-        }
-    }
-#if !defined(DF_YPASS_NOWINDOW)
-    if (TABLE && !PC && YU < 4 && Nlo == Nhi && a.ywindow && t + 5 <= bh) {
-        // Table mode, one N for the whole tile (every tile of a row-uniform plane except where N
-        // steps): tap t of row r uses b[t - r], so the 4 taps t..t+3 of all R rows need only the
-        // R + 3 coefficients b[t-R+1 .. t+3], one s_load_dwordx16 window; the next iteration's
-        // window is loaded one iteration ahead so the scalar loads never stall the taps.
-        // Same products, same order: bit-identical to the per-row path.
-        constexpr int WN = (R + 3 + 7) / 8 * 8;
-        const double *cb = tb[0] - (R - 1); // window base: b[t - R + 1 + k] = cb[t + k]
-        double cw[WN];
-#pragma unroll
-        for (int k = 0; k < WN; ++k) cw[k] = DF_TCOEF(cb[t + k]);
-        double2 n0 = noise(t), n1 = noise(t + 1);
-        auto tap = [&](int u, const double2 n) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const double b = cw[u - r + R - 1];
-                acc0[r] += b * n.x;
-                acc1[r] += b * n.y;
-            }
-        };
-        for (; t + 5 <= bh; t += 4) {
-            double cn[WN];
-#pragma unroll
-            for (int k = 0; k < WN; ++k) cn[k] = DF_TCOEF(cb[t + 4 + k]); // the table is padded past its last vector
-            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
-            tap(0, n0);
-            tap(1, n1);
-            n0 = noise(t + 4);
-            n1 = noise(t + 5);
-            tap(2, m0);
-            tap(3, m1);
-#pragma unroll
-            for (int k = 0; k < WN; ++k) cw[k] = cn[k];
-        }
-        // t + 1 <= bh still holds (n0, n1 are rows t, t + 1): finish in the per-row loops below
-        for (; t + 1 <= bh; t += 2) {
-            body_n(t, n0);
-            body_n(t + 1, n1);
-            if (t + 3 <= bh) {
-                n0 = noise(t + 2);
-                n1 = noise(t + 3);
-            }
-        }
-    }
-#endif
-    if (kPrefetch && TABLE && !PC && YU < 4 && t + 1 <= bh) {
-        // VALU-bound table mode: the next two noise rows are in flight while this pair's
-        // taps run (the compiler would wait on each iteration's own loads)
-        // (two register pairs in ping-pong: no copies, so no wait at the end of an iteration)
-        double2 n0 = noise(t), n1 = noise(t + 1);
-        for (; t + 5 <= bh; t += 4) {
-            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
-            body_n(t, n0);
-            body_n(t + 1, n1);
-            n0 = noise(t + 4);
-            n1 = noise(t + 5);
-            body_n(t + 2, m0);
-            body_n(t + 3, m1);
-        }
-        if (t + 3 <= bh) {
-            const double2 m0 = noise(t + 2), m1 = noise(t + 3);
-            body_n(t, n0);
-            body_n(t + 1, n1);
-            body_n(t + 2, m0);
-            body_n(t + 3, m1);
-            t += 4;
-        } else {
-            body_n(t, n0);
-            body_n(t + 1, n1);
-            t += 2;
-        }
-    }
     if (YU >= 4) {
         for (; t + 3 <= bh; t += 4) {
             body(t);
@@ -1740,14 +1319,7 @@ __global__ __launch_bounds__(256) DF_YPASS_ATTR void ypass_kernel(SweepArgs a, i
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < nr) {
-#if defined(DF_STORE_SINK)
-            double *o = a.rz[c] + a.Nzp[c] + col; // timing only: all rows onto row 0
-#else
             double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + col;
-#endif
-#if defined(DF_ABLATE_STORE)
-            if (acc0[r] != 1234.5) continue; // timing only
-#endif
             if (col + 1 < a.Nz_loc) {
                 if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
                 else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
@@ -1801,14 +1373,14 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
     double acc0[R], acc1[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc0[r] = acc1[r] = 0.0;
-    auto noise = [&](int t) { return DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz), t); };
+    auto noise = [&](int t) { return ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)t * Pz)); };
     auto predicated = [&](int t) {
         const double2 n = noise(t);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int i = t - r;
             if (r < nr && i >= -N[r] && i <= N[r]) {
-                const double bb = DF_TCOEF(tb[r][i]);
+                const double bb = tb[r][i];
                 acc0[r] += bb * n.x;
                 acc1[r] += bb * n.y;
             }
@@ -1817,7 +1389,7 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
     auto body_n = [&](int t, const double2 n) {
         double bb[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) bb[r] = DF_TCOEF(tb[r][t - r]);
+        for (int r = 0; r < R; ++r) bb[r] = tb[r][t - r];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             acc0[r] += bb[r] * n.x;
@@ -1837,10 +1409,10 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
         const ptrdiff_t P1 = Pz, P2 = 2 * (ptrdiff_t)Pz, P3 = 3 * (ptrdiff_t)Pz, P4 = 4 * (ptrdiff_t)Pz;
         const double *nl = np + (ptrdiff_t)t * Pz; // next group to load
         auto ldn = [&](double2 (&nn)[4]) {
-            nn[0] = DF_NOISE(reinterpret_cast<const double2 *>(nl), 0);
-            nn[1] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P1), 1);
-            nn[2] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P2), 2);
-            nn[3] = DF_NOISE(reinterpret_cast<const double2 *>(nl + P3), 3);
+            nn[0] = ld_pair(reinterpret_cast<const double2 *>(nl));
+            nn[1] = ld_pair(reinterpret_cast<const double2 *>(nl + P1));
+            nn[2] = ld_pair(reinterpret_cast<const double2 *>(nl + P2));
+            nn[3] = ld_pair(reinterpret_cast<const double2 *>(nl + P3));
             nl += P4;
         };
         auto taps = [&](const double2 (&nn)[4], const double (&ww)[WN]) {
@@ -1858,7 +1430,7 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
         const double *wq = cb + t;
         double w[WN];
 #pragma unroll
-        for (int k = 0; k < WN; ++k) w[k] = DF_TCOEF(wq[k]);
+        for (int k = 0; k < WN; ++k) w[k] = wq[k];
 #pragma unroll
         for (int g = 0; g < KYD; ++g) ldn(nq[g]);
         for (; t + 8 * KYD - 1 <= bh; t += 4 * KYD) { // the groups issued below stay within bh
@@ -1866,7 +1438,7 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
             for (int g = 0; g < KYD; ++g) {
                 double wn[WN];
 #pragma unroll
-                for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]); // the table is padded past its last vector
+                for (int k = 0; k < WN; ++k) wn[k] = wq[4 + k]; // the table is padded past its last vector
                 __builtin_amdgcn_sched_barrier(0);
                 taps(nq[g], w);
                 ldn(nq[g]); // group t + 4 (g + KYD)
@@ -1880,7 +1452,7 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
         for (int g = 0; g < KYD; ++g) { // drain: groups t .. t + 4 KYD - 1, loaded, within bh
             double wn[WN];
 #pragma unroll
-            for (int k = 0; k < WN; ++k) wn[k] = DF_TCOEF(wq[4 + k]);
+            for (int k = 0; k < WN; ++k) wn[k] = wq[4 + k];
             taps(nq[g], w);
             wq += 4;
 #pragma unroll
@@ -1955,12 +1527,6 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     const int x = blockIdx.x & 7;
     const int pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
     if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
-#if defined(DF_COOP2_ONLY_XCD)
-    if (x != DF_COOP2_ONLY_XCD) return; // timing only: one XCD's run alone
-#endif
-#if defined(DF_COOP2_SKIP_XCD)
-    if (x == DF_COOP2_SKIP_XCD) return; // timing only: every run but one XCD's
-#endif
     const int tile = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos;
     const int s = tile / nrowblk;             // rows ascending within a strip (L2 reuse of noise rows)
     const int j0 = (tile - s * nrowblk) * RR;
@@ -1993,7 +1559,7 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
 #pragma unroll
         for (int k = 0; k < KPW; ++k) {
             const int u = u0 + (w + 4 * k) * G + q, m = mlo + u;
-            n[k] = (live && u < M) ? DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)u * a.Pz), u)
+            n[k] = (live && u < M) ? ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)u * a.Pz))
                                       : make_double2(0.0, 0.0);
 #pragma unroll
             for (int r = 0; r < RR; ++r)
@@ -2030,11 +1596,6 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
                 const int ua = __builtin_amdgcn_readfirstlane(max(0, lor[i] - mlo - u0));
                 const int ub = __builtin_amdgcn_readfirstlane(min(CHG, hir[i] - mlo - u0 + 1));
                 const double *pc = reinterpret_cast<const double *>(prod + (2 * i + rs) * CH * 64) + cell;
-#if defined(DF_COOP2_SERIAL_SUM)
-                for (int u = ua; u < ub; ++u) acc[i] += pc[u * 2 * P]; // timing only: one LDS round trip per add
-#elif defined(DF_ABLATE_COOPSUM)
-                if (ua < ub) acc[i] += pc[ua * 2 * P]; // timing only: one product per chunk
-#else
                 // LDS reads issued 8 at a time, then their adds in tap order: one add per LDS round trip made
                 // the sum a serial chain of LDS latencies (CHG = 128 of them per chunk on a folded narrow strip).
                 if (P == 64 && ua == 0 && ub == CHG) { // whole chunk of a full strip: immediate offsets
@@ -2057,7 +1618,6 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
                             if (g + e < ub) acc[i] += v[e]; // wave-uniform condition
                     }
                 }
-#endif
             }
         }
         __syncthreads();
@@ -2130,7 +1690,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 #pragma unroll
         for (int k = 0; k < LW; ++k) {
             const int m = u0 + w + NW * k;
-            pre[k0][k] = live && m <= mhi ? DF_NOISE(reinterpret_cast<const double2 *>(np + (ptrdiff_t)m * a.Pz), m)
+            pre[k0][k] = live && m <= mhi ? ld_pair(reinterpret_cast<const double2 *>(np + (ptrdiff_t)m * a.Pz))
                                           : make_double2(0.0, 0.0);
         }
     };
@@ -2159,7 +1719,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
                 const double2 n = nbuf[buf][q][lane];
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const double b = DF_TCOEF(cb[r][q]);
+                    const double b = cb[r][q];
                     acc0[r] += b * n.x;
                     acc1[r] += b * n.y;
                 }
@@ -2170,7 +1730,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 #pragma unroll
                 for (int r = 0; r < R; ++r)
                     if (m >= lo[r] && m <= hi[r]) { // wave-uniform
-                        const double b = DF_TCOEF(tb[r][m - lo[r]]);
+                        const double b = tb[r][m - lo[r]];
                         acc0[r] += b * n.x;
                         acc1[r] += b * n.y;
                     }
@@ -2359,14 +1919,9 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     if constexpr (TABLE) {
         if (a.per_cell) {
             hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, true>), grid, dim3(256), 0, st, a, nrowblk);
-        } else if (a.ydepth >= 1) {
+        } else {
             constexpr int KYD = R <= 2 ? 4 : R == 4 ? 2 : 1;
-            if (a.ydepth >= 2 && R == 4) // timing: 3 groups ahead at 4 rows
-                hipLaunchKernelGGL((ypass_table_kernel<R, 3>), grid, dim3(256), 0, st, a, nrowblk);
-            else
-                hipLaunchKernelGGL((ypass_table_kernel<R, KYD>), grid, dim3(256), 0, st, a, nrowblk);
-        } else { // ydepth 0: the shared ypass_kernel (A/B only)
-            hipLaunchKernelGGL((ypass_kernel<R, true, false, 2, false>), grid, dim3(256), 0, st, a, nrowblk);
+            hipLaunchKernelGGL((ypass_table_kernel<R, KYD>), grid, dim3(256), 0, st, a, nrowblk);
         }
     } else if (a.yunroll >= 8) {
         hipLaunchKernelGGL((ypass_kernel<R, false, true, 8, false>), grid, dim3(256), 0, st, a, nrowblk);
@@ -2518,25 +2073,22 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         auto coef = [&](int t) -> double2 {
             if (TABLE) {
                 if (!PC) {
-                    const double v = DF_TCOEF(tb[t]);
+                    const double v = tb[t];
                     return make_double2(v, v);
                 }
                 const int i = t - N, ai = i < 0 ? -i : i;
-                return make_double2(DF_TCOEF(tb[ai]), DF_TCOEF(tb1[ai]));
+                return make_double2(tb[ai], tb1[ai]);
             }
             return ldB<NT>(bp + (ptrdiff_t)t * kStrip);
         };
         // one instantiation per address space: global (plain loads) or LDS (ds_read_b128)
         auto taps = [&](auto xp, double &r0, double &r1) {
         double acc0 = 0.0, acc1 = 0.0;
-        double2 P = DF_NOISE(xp, 0);
+        double2 P = ld_pair(xp);
         int m = 0;
         if (ZU >= 4) {
-#if defined(DF_ZPASS_UNROLL1)
-#pragma unroll 1
-#endif
             for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
-                const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2), P3 = DF_NOISE(xp + m + 3, m + 3), P4 = DF_NOISE(xp + m + 4, m + 4);
+                const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2), P3 = ld_pair(xp + m + 3), P4 = ld_pair(xp + m + 4);
                 double2 b[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) b[u] = coef(2 * m + u);
@@ -2560,7 +2112,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             }
         }
         for (; m + 2 <= N; m += 2) {
-            const double2 P1 = DF_NOISE(xp + m + 1, m + 1), P2 = DF_NOISE(xp + m + 2, m + 2);
+            const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2);
             const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
             acc0 += b0.x * P.x;
             acc1 += b0.y * P.y;
@@ -2573,7 +2125,7 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
             P = P2;
         }
         for (; m < N; ++m) {
-            const double2 P1 = DF_NOISE(xp + m + 1, m + 1);
+            const double2 P1 = ld_pair(xp + m + 1);
             const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1);
             acc0 += b0.x * P.x;
             acc1 += b0.y * P.y;
@@ -2627,20 +2179,13 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
     const double t1 = rc[4 * Ny + j], Ts = rc[5 * Ny + j], rh = rc[6 * Ny + j];
     // The lane's two cells as one 16-B access per field when the row offset keeps them
     // aligned (every row when Nz_loc is even), else two 8-B accesses.
-#if defined(DF_STORE_SINK)
-    const size_t idx = (size_t)col; // timing only: every row lands on row 0 (stores stay in L2)
-#else
     const size_t idx = (size_t)j * a.Nz_loc + col;
-#endif
     const bool has1 = col + 1 < a.Nz_loc, pair = has1 && (idx & 1) == 0;
     auto ld = [&](const double *p) -> double2 {
         if (pair) return *reinterpret_cast<const double2 *>(p + idx);
         return make_double2(p[idx], has1 ? p[idx + 1] : 0.0);
     };
     auto st = [&](double *p, double x, double y) {
-#if defined(DF_ABLATE_STORE)
-        if (x != 1234.5) return; // timing only: keep the values live, store nothing
-#endif
         if (pair) {
             if (a.nt_stores) __builtin_nontemporal_store(dvec2{x, y}, reinterpret_cast<dvec2 *>(p + idx));
             else *reinterpret_cast<double2 *>(p + idx) = make_double2(x, y);

@@ -49,7 +49,7 @@ struct WaveTask {
     int gw, pad;
 };
 
-// K3a / K3r destination of a 128-position chunk (host-built, RngGeom::chunk_dest): position i of the chunk, if
+// K3r destination of a 128-position chunk (host-built, RngGeom::chunk_dest): position i of the chunk, if
 // lo <= i < hi, goes to buffer arr + off + i, plus jump once i >= wr (one row wrap: pitch - width); positions
 // outside [lo, hi) are drawn but not stored here (other strips' columns, the r_zs interior).
 struct ChunkDest {
@@ -89,16 +89,9 @@ struct RngGeom {
     uint64_t inv_width[6];         // ceil(2^64 / width): row = umulhi(p, inv) for p < 2^32 (0 if width == 1)
     int Nzp[3], rz_pitch[3];
     double *ry[3], *rz[3];
-    // Dense generation (gen_dense): Kc writes the start state of every accepted attempt whose 64-rank
-    // chunk stores something here to cstate[rank]; K3a runs a wave per 8 such chunks (the host's list for
-    // the call's parity f = incoming saved_flag), a lane per rank.
-    int gen_dense;                  // 1: Kc + K3a; 2: run generation (K2s, K3r)
-    uint64_t *cstate;               // [64 * chunk count]
-    const uint32_t *need_bits[2];   // bitmap over chunks (+ 2 padding words), per parity f
-    const uint32_t *chunks[2];      // needed chunk ids in increasing order, per parity f
-    int nchunks[2];
-    // K3a fast chunks (one GPU): per listed chunk, where its 128 positions land when they all go to one r_ys
-    // array with at most one row wrap; arr < 0 marks a chunk for the general per-lane path.
+    int gen_dense;                  // 0: compacted K3; 2: run generation (K2s, K3r)
+    // K3r fast chunks: per listed needed chunk of the call's parity f, where its 128 positions land when they all
+    // go to one stream array with at most one row wrap; arr < 0 marks a chunk for the general per-lane path.
     const struct ChunkDest *chunk_dest[2];
     // Run generation (gen_dense 2). The attempt blocks are cut into xworld shares of xchunk blocks (the z-strip
     // ranks' counting shares; one share on a single GPU); share s has a record of xstride bytes at xbuf +
@@ -148,7 +141,6 @@ struct SweepArgs {
     int ycoop2_xcd[3][9];   // row-pair y-pass: XCD x runs tiles [ycoop2_xcd[c][x], ycoop2_xcd[c][x+1]) (equal bytes)
     int ycoop2_run;         // the longest such run (grid = 8 x this)
     const int *ycoop2_perm[3]; // dispatch position -> tile inside each run (nullptr: ascending)
-    int ydepth;                // table y-pass: 1 ypass_table_kernel (2: 3 noise groups ahead at 4 rows); 0 the shared kernel
     int ylds;                  // table y-pass with the noise staged in LDS per block of 4R rows (ypass_tlds_kernel)
     // ylds 3 (ypass_t64_kernel): blocks of 4 ylist_R rows x 64 columns, launched in the order ylist[0, ylist_n)
     // (tile = (c * ylist_ncol + column tile) * ylist_nrb + row block; heaviest union of noise rows first)
@@ -163,8 +155,6 @@ struct SweepArgs {
     const int *halo_w[3];
     const long long *halo_off[3];
     int zgroup;             // table z-pass: blocks of (row, <= 4 consecutive strips) (launches without a gap)
-    int ywindow;            // shared y-pass kernel, table mode (ydepth 0): prefetched coefficient windows
-    int ydeep;              // shared y-pass kernel, table mode (ydepth 0): loads a whole 4-tap group ahead
     int zstage_reg;         // doubles per component region of that LDS segment (512 + 2 * max Nzp)
     // Write windows: a wave holds its output stores until the chip-wide real-time clock (100 MHz) is
     // in the first W ticks of a T-tick period, so the CUs write together and the read stream runs

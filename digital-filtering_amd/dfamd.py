@@ -13,7 +13,7 @@ import sys
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# DFAMD_LIB: a timing-only kernel variant (Makefile `variant` target, tools/variant_ab.sh)
+# DFAMD_LIB: another build of the library, for same-box A/B timing (tools/lib_ab.sh)
 LIB_PATH = os.environ.get("DFAMD_LIB") or os.path.join(HERE, "libdfamd.so")
 DATA = os.path.join(HERE, "data")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "df_c.h")
@@ -209,7 +209,12 @@ def make_config(plane="native", Ny=0, Nz=0, N_min=0, N_max=0, seed=None, coeff_m
 class DigitalFilter:
     """DIGITAL_FILTER(DFConfig): setup + constructor step 0 on the GPU."""
 
-    def __init__(self, _handle=None, _keep=None, **kw):
+    # keys that change how the noise is generated: the generations prefetched at create are redrawn after them
+    RNG_FORM_KEYS = ("gen_dense", "gen_split", "fuse_plan", "fast_log")
+
+    def __init__(self, _handle=None, _keep=None, tuning=None, **kw):
+        """tuning: df_set_tuning keys applied right after create (step 0 has run with the plane's defaults;
+        noise already prefetched is redrawn when a generation-form key is among them)."""
         if _handle is not None:
             self._h, self._keep = _handle, _keep
         else:
@@ -222,6 +227,11 @@ class DigitalFilter:
         _check(lib().df_dims(self._h, C.byref(ny), C.byref(nz), C.byref(z0), C.byref(z1)))
         self.Ny, self.Nz, self.z0, self.z1 = ny.value, nz.value, z0.value, z1.value
         self.Nz_loc = self.z1 - self.z0
+        if tuning:
+            for k, v in tuning.items():
+                self.set_tuning(k, v)
+            if any(k in self.RNG_FORM_KEYS for k in tuning):
+                self.set_rng_state(*self.rng_state())  # restart the noise pipeline with the new form
 
     def close(self):
         if getattr(self, "_h", None):
@@ -401,8 +411,9 @@ class DigitalFilter:
         return lib().df_algorithmic_bytes(self._h, kernel)
 
 
-def create_group(n, **kw):
-    """n z-strips of one plane in this process (in-process halo copies)."""
+def create_group(n, tuning=None, **kw):
+    """n z-strips of one plane in this process (in-process halo copies). tuning: df_set_tuning keys for every
+    strip, from the call after the generation prefetched at create on."""
     cfgs = (_Cfg * n)()
     keep = []
     for r in range(n):
@@ -411,7 +422,11 @@ def create_group(n, **kw):
         keep += k
     hs = (C.c_void_p * n)()
     _check(lib().df_create_group(cfgs, n, hs))
-    return [DigitalFilter(_handle=hs[r], _keep=keep) for r in range(n)]
+    out = [DigitalFilter(_handle=hs[r], _keep=keep) for r in range(n)]
+    for f in out:
+        for k, v in (tuning or {}).items():
+            f.set_tuning(k, v)
+    return out
 
 
 def filter_group(filters, dt):

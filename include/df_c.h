@@ -208,32 +208,35 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  * 2 (default) = glibc's own log algorithm in the polar transform (normals and fields bit-identical to
  * the reference's), 1 = a table-driven log within 1 ulp of it, 0 = the device math library's log;
  * 1 and 0 keep the normals within 2 ulp of the reference's). Every key is a default on some plane or a
- * documented use; variants measured neutral or slower were removed in round 4.
+ * documented use; variants measured neutral or slower were removed (rounds 4-5, DESIGN.md sections 8-9).
+ * Sweeps:
  *   "rows_per_wave" (1,2,4,8; 0 at create = by plane), "yunroll" (packed per-wave y-pass: 2, 4; 8 = the
- *   8-deep load ring of long chains), "zunroll" (2,4), "ycoop" (packed y-pass: 7 = a block per row pair,
- *   the long-chain default; 0 = a wave per tile), "ycoop_order" (row-pair dispatch inside each XCD run:
- *   0 ascending, g >= 1 groups of g tiles heaviest first; 4 on long chains), "ycoop_ovh" (XCD balance
- *   per-tile cost), "ylds" (table y-pass with LDS-staged noise: long-chain default; 0 off),
- *   "ydepth" (table y-pass: 1 its own kernel; 2 three noise groups ahead at 4 rows; 0 the shared kernel,
- *   with "ydeep" / "ywindow"), "zsplit" (packed z-pass, a wave per component: few-tile planes),
- *   "zstage" (table z-pass noise staged in LDS: 2 default, 0 off), "nt_stores" / "znt_stores" /
- *   "ynt_stores" / "rng_nt_stores" (non-temporal stores), "ywin_T" / "ywin_W" / "zwin_T" / "zwin_W"
- *   (sweep write windows), "gen_split" (1-16: noise-generation waves per wave of attempts, small
- *   planes), "fuse_plan" (K3 plans its own waves on small planes), "handoff_batch" (1,2,4: generations
- *   per cross-stream hand-off), "gen_dense" (0 compacted K3; 1 Kc + K3a; 2 run generation: group
- *   counts, one wave per piece of needed chunks), "k3a_fast" (host-built chunk destinations),
- *   "fused_exchange" (split counting with gen_dense 2: the next generation's share records travel in
- *   the call's halo group, one grouped RCCL operation per call; 0 = an all-gather of their own),
- *   "rng_replicate" (z-strips: 1 every rank counts every attempt, 0 split counting), "halo_overlap"
- *   (RCCL z-strips: 1 = send/recv, unpack and edge-strip z-pass on a high-priority stream under the
- *   interior strips' z-pass; 0 = one serial chain; -1 default = 1 packed, 0 table), "halo_loopback"
- *   (one-rank RCCL handle: send the halo to itself and check it), "fast_log" (above). */
+ *   8-deep load ring of long chains), "ycoop" (packed y-pass: 7 = a block per row pair, the long-chain
+ *   default; 0 = a wave per tile), "ycoop_order" (row-pair dispatch inside each XCD run: 0 ascending,
+ *   g >= 1 groups of g tiles heaviest first; 4 on long chains), "ylds" (table y-pass with LDS-staged noise:
+ *   2 = a block per (strip, 4 rows), 3 = a block per (64 columns, 4 "yt_rows" rows), heaviest first;
+ *   0 = a wave per tile), "yt_rows" (1, 2, 4, 8: rows per wave of ylds 3), "zsplit" (packed z-pass, a wave
+ *   per component: few-tile planes), "zstage" (table z-pass noise staged in LDS: 2 default, 0 the unstaged
+ *   form large halos take), "nt_stores" (non-temporal output stores), "ywin_T" / "ywin_W" / "zwin_T" /
+ *   "zwin_W" (sweep write windows: packed planes streaming >= 2 GB of coefficients).
+ * Noise generation:
+ *   "gen_split" (1-16: generation waves per wave of attempts, small planes), "fuse_plan" (the compacted K3
+ *   plans its own waves on small planes), "handoff_batch" (1,2,4: generations per cross-stream hand-off;
+ *   at most half the noise sets allocated at create), "gen_dense" (0 compacted K3; 2 run generation:
+ *   group counts, one wave per piece of needed chunks), "fast_log" (above).
+ * Z-strips (RCCL handles; "gen_dense", "fused_exchange" and "rng_replicate" change the collective sequence:
+ * set them alike on every rank before the next df_filter):
+ *   "rng_replicate" (1 every rank counts every attempt, 0 split counting), "fused_exchange" (split
+ *   counting with gen_dense 2: the next generation's share records travel in the call's halo group, one
+ *   grouped RCCL operation per call; 0 = an all-gather of their own), "halo_overlap" (1 = send/recv, unpack
+ *   and edge-strip z-pass on a high-priority stream under the interior strips' z-pass; 0 = one serial
+ *   chain; -1 default = 1 packed, 0 table), "halo_loopback" (one-rank RCCL handle: send the halo to itself
+ *   and check it). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* The launch shape the handle will use for a df_set_tuning key: the plane-dependent defaults chosen at
- * create time (host-only handles included) or the last setting. Keys: "rows_per_wave", "yunroll",
- * "zunroll", "ycoop", "ycoop_order", "ydepth", "ylds", "handoff_batch", "halo_overlap", "gen_dense",
- * "k3a_fast", "fused_exchange". DF_EINVAL for other keys. */
+ * create time (host-only handles included) or the last setting. Every df_set_tuning key but
+ * "halo_loopback"; DF_EINVAL for other keys. */
 int df_get_tuning(df_handle *h, const char *key, int *value);
 
 /* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every

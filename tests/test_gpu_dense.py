@@ -1,10 +1,9 @@
-"""Dense noise generation (RngGeom::gen_dense, round 3: Kc compacts the accepted attempts' states into
-memory by rank, K3a runs one wave per needed 64-rank chunk, K3b evaluates glibc's near-1 log band
-apart). It is the table-mode default on planes of more than 1024 attempt blocks and on split planes;
-here it is forced on small planes (DFAMD_GEN_DENSE=1, DFAMD_GEN_SPLIT=1, DFAMD_FUSE_PLAN=0 at create)
-and checked bit for bit against the oracle: fields, the stream state after every call, the six noise
-arrays, both parities of the carried normal (f = 0 and a resumed f = 1), z-strip groups, and packed
-mode."""
+"""Chunk generation through the run form (RngGeom::gen_dense 2: one wave per piece of needed 64-rank chunks,
+glibc's near-1 log band evaluated apart) forced on small planes that otherwise take the compacted K3
+(tuning gen_dense 2, gen_split 1, fuse_plan 0, applied after create; the noise prefetched at create is
+redrawn), checked bit for bit against the oracle: fields, the stream state after every call, the six noise
+arrays, both parities of the carried normal (f = 0 and a resumed f = 1), z-strip groups, and packed mode.
+(Round 3's two-kernel dense form, Kc + K3a, was removed in round 5; these cases now pin the run form.)"""
 import numpy as np
 import pytest
 
@@ -13,13 +12,7 @@ import oracle as O
 
 pytestmark = pytest.mark.gpu
 FIELDS = ("u", "v", "w", "T", "rho")
-
-
-@pytest.fixture
-def dense_env(monkeypatch):
-    monkeypatch.setenv("DFAMD_GEN_DENSE", "1")
-    monkeypatch.setenv("DFAMD_GEN_SPLIT", "1")
-    monkeypatch.setenv("DFAMD_FUSE_PLAN", "0")
+RUN = dict(gen_dense=2, gen_split=1, fuse_plan=0)
 
 
 def synth(Ny, Nz, lo, hi, **kw):
@@ -35,11 +28,11 @@ def start_state(seed, flag):
 @pytest.mark.parametrize("flag", [0, 1])
 @pytest.mark.parametrize("mode", ["table", "packed"])
 @pytest.mark.parametrize("spec", [(128, 128, 8, 8), (37, 5, 2, 10), (70, 129, 2, 6), (96, 300, 4, 20), (2, 1, 2, 2)])
-def test_dense_fields_bitexact_vs_oracle(dense_env, spec, mode, flag):
+def test_dense_fields_bitexact_vs_oracle(spec, mode, flag):
     st = start_state(3 + flag, flag)
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3],
                  rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))
-    g = synth(*spec, resume=st, coeff_mode=mode)
+    g = synth(*spec, resume=st, coeff_mode=mode, tuning=RUN)
     for dt in (None, 1e-8, 1e-8, 1e-5):
         if dt is not None:
             o.filter(dt)
@@ -51,12 +44,12 @@ def test_dense_fields_bitexact_vs_oracle(dense_env, spec, mode, flag):
 
 
 @pytest.mark.parametrize("flag", [0, 1])
-def test_dense_noise_arrays_bitexact(dense_env, flag):
+def test_dense_noise_arrays_bitexact(flag):
     spec = (64, 200, 2, 12)
     st = start_state(11, flag)
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=64, Nz=200, N_min=2, N_max=12,
                  rng=O.Rng(state=st[0], saved_flag=st[1], saved=st[2]))
-    g = synth(*spec, resume=st, coeff_mode="table")
+    g = synth(*spec, resume=st, coeff_mode="table", tuning=RUN)
     for _ in range(2):
         o.filter(1e-8)
         g.filter(1e-8)
@@ -69,10 +62,10 @@ def test_dense_noise_arrays_bitexact(dense_env, flag):
 
 
 @pytest.mark.parametrize("world,Nz", [(2, 300), (3, 700)])
-def test_dense_strip_groups_match_whole(dense_env, world, Nz):
+def test_dense_strip_groups_match_whole(world, Nz):
     spec = dict(plane="synthetic", Ny=100, Nz=Nz, N_min=4, N_max=16, seed=8, device=0, coeff_mode="table")
-    whole = dfamd.DigitalFilter(**spec)
-    strips = dfamd.create_group(world, **spec)
+    whole = dfamd.DigitalFilter(tuning=RUN, **spec)
+    strips = dfamd.create_group(world, tuning=RUN, **spec)
     for _ in range(3):
         whole.filter(1e-8)
         dfamd.filter_group(strips, 1e-8)
@@ -83,12 +76,12 @@ def test_dense_strip_groups_match_whole(dense_env, world, Nz):
 
 
 def test_dense_and_compact_forms_agree_when_switched():
-    # the default table plane switched between the dense and the compacted K3 between calls
+    # the default table plane switched between the run form and the compacted K3 between calls
     spec = (200, 300, 4, 24)
     a = synth(*spec, seed=21, coeff_mode="table")
     b = synth(*spec, seed=21, coeff_mode="table")
-    for kw in (dict(fuse_plan=0, gen_split=1, gen_dense=1), dict(gen_dense=0), dict(gen_dense=1),
-               dict(fuse_plan=1, gen_dense=1), dict(fuse_plan=0, gen_split=2, gen_dense=1)):
+    for kw in (dict(fuse_plan=0, gen_split=1, gen_dense=2), dict(gen_dense=0), dict(gen_dense=2),
+               dict(fuse_plan=1, gen_dense=2), dict(fuse_plan=0, gen_split=2, gen_dense=2)):
         for k, v in kw.items():
             b.set_tuning(k, v)
         a.filter(1e-8)

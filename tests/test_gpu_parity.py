@@ -82,13 +82,12 @@ def test_rng_stream_state_bitexact(spec):
 
 
 @pytest.mark.parametrize("fast_log", ["2", "1", "0"])
-def test_noise_arrays_match_oracle(monkeypatch, fast_log):
+def test_noise_arrays_match_oracle(fast_log):
     # fast_log 2 (default): glibc's own log (df_rng.hpp glibc_log): the normals are the reference's bits;
     # 1: the table-driven log_r2; 0: the device library's log (both within 2 ulp)
-    monkeypatch.setenv("DFAMD_FAST_LOG", fast_log)
     spec = (64, 200, 2, 12)
     o = oracle_synth(*spec, seed=11)
-    g = gpu_synth(*spec, seed=11)
+    g = gpu_synth(*spec, seed=11, tuning=dict(fast_log=int(fast_log)))
     o.filter(1e-8)
     g.filter(1e-8)
     diff_ulps = []
@@ -166,8 +165,9 @@ def test_golden_c2_bitexact_vs_reference(mode):
 
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(rows_per_wave=1, yunroll=8, ycoop=0)),
-                                         ("packed", dict(zsplit=1)), ("packed", dict(ycoop=7, ycoop_ovh=64)),
-                                         ("table", dict(ylds=0, rows_per_wave=4)), ("table", dict(gen_dense=2))])
+                                         ("packed", dict(zsplit=1)), ("packed", dict(ycoop=7, ycoop_order=1)),
+                                         ("table", dict(ylds=0, rows_per_wave=4)), ("table", dict(gen_dense=2)),
+                                         ("table", dict(ylds=3, yt_rows=2))])
 def test_golden_native_grid(mode, tuning):
     # the reference's own grid (N_y up to 212): default shapes and the deep y-pass pipeline
     g = np.load(os.path.join(GOLDEN, "native_s42.npz"))
@@ -187,12 +187,12 @@ def test_golden_native_grid(mode, tuning):
 
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=0)), ("packed", dict(ycoop_order=1)),
                                          ("packed", dict(ycoop_order=8)),
-                                         ("table", {}), ("table", dict(ydepth=0)), ("table", dict(rows_per_wave=1)),
+                                         ("table", {}), ("table", dict(rows_per_wave=1)),
                                          ("table", dict(ylds=1)), ("table", dict(ylds=2, rows_per_wave=2)),
                                          ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
                                          ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
                                          ("table", dict(ylds=3, yt_rows=8)),
-                                         ("table", dict(ylds=0, ydepth=0))])
+                                         ("table", dict(ylds=0))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
     # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
@@ -310,16 +310,13 @@ def test_runtime_tuning_is_bitexact(mode):
     spec = (131, 260, 2, 16)
     a = gpu_synth(*spec, seed=5, coeff_mode=mode)
     b = gpu_synth(*spec, seed=5, coeff_mode=mode)
-    settings = [dict(rows_per_wave=1, zunroll=4, yunroll=4), dict(rows_per_wave=8),
-                dict(rows_per_wave=2, zunroll=2, yunroll=2, nt_stores=1), dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8),
+    settings = [dict(rows_per_wave=1, yunroll=4), dict(rows_per_wave=8),
+                dict(rows_per_wave=2, yunroll=2, nt_stores=1), dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8),
                 dict(rows_per_wave=4, yunroll=8), dict(gen_split=1), dict(gen_split=4), dict(gen_split=16),
                 dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256), dict(ywin_T=0, zwin_T=4096, zwin_W=0),
-                dict(gen_split=2), dict(zsplit=1), dict(zsplit=0), dict(ycoop=7), dict(ycoop=7, ycoop_ovh=64),
-                dict(ycoop_ovh=0), dict(ycoop=7, ycoop_order=1), dict(ycoop=7, ycoop_order=4), dict(ycoop_order=0),
-                dict(ycoop=0, yunroll=2), dict(ydepth=1, rows_per_wave=2), dict(ydepth=2, rows_per_wave=4),
-                dict(ydepth=1, rows_per_wave=1), dict(ydepth=1, rows_per_wave=8), dict(ydepth=0, ydeep=1, ywindow=0),
-                dict(ydepth=0, ywindow=1, rows_per_wave=2), dict(ydepth=1), dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=0),
-                dict(fuse_plan=0, gen_split=1, gen_dense=1, k3a_fast=1), dict(fuse_plan=0, gen_split=1, gen_dense=2),
+                dict(gen_split=2), dict(zsplit=1), dict(zsplit=0), dict(ycoop=7), dict(ycoop=7, ycoop_order=1), dict(ycoop=7, ycoop_order=4), dict(ycoop_order=0),
+                dict(ycoop=0, yunroll=2), dict(rows_per_wave=2), dict(rows_per_wave=1), dict(rows_per_wave=8),
+                dict(fuse_plan=0, gen_split=1, gen_dense=2),
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
@@ -345,13 +342,12 @@ def test_runtime_tuning_is_bitexact(mode):
 
 
 @pytest.mark.parametrize("hb", ["1", "2", "4"])
-def test_handoff_batch_mid_epoch_state_changes(monkeypatch, hb):
+def test_handoff_batch_mid_epoch_state_changes(hb):
     # epochs of hb calls over 2*hb noise sets: a stream state set mid-epoch, the stage API and filter calls
     # interleaved, checked against the oracle after every step
-    monkeypatch.setenv("DFAMD_HANDOFF_BATCH", hb)
     spec = (48, 96, 2, 10)
     o = oracle_synth(*spec, seed=13)
-    g = gpu_synth(*spec, seed=13)
+    g = gpu_synth(*spec, seed=13, tuning=dict(handoff_batch=int(hb)))
     # a loaded state drops the handle to one generation per epoch; 16 calls later it batches again
     # (kHbRestoreCalls): loads at calls 2, 3 and 22 cover the drop, the return and a drop after it
     for i in range(26):
@@ -367,12 +363,10 @@ def test_handoff_batch_mid_epoch_state_changes(monkeypatch, hb):
 
 @pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90), (37, 129, 2, 10), (40, 133, 2, 8)])
 def test_dense_fast_chunks_match_oracle(spec):
-    # K3a's fast chunks (host-built destinations, ChunkDest) forced through the dense generation on small planes:
-    # odd and even widths (row wraps inside a chunk, odd wrap points), both parities of the carried normal
+    # the run generation's fast chunks (host-built destinations, ChunkDest) forced on small planes: odd and even
+    # widths (row wraps inside a chunk, odd wrap points), both parities of the carried normal
     o = oracle_synth(*spec, seed=29)
-    g = gpu_synth(*spec, seed=29, coeff_mode="table")
-    for k, v in (("gen_split", 1), ("fuse_plan", 0), ("gen_dense", 1)):
-        g.set_tuning(k, v)
+    g = gpu_synth(*spec, seed=29, coeff_mode="table", tuning=dict(gen_split=1, fuse_plan=0, gen_dense=2))
     flags = set()
     for i in range(5):
         o.filter(1e-8)
@@ -404,7 +398,7 @@ def test_random_planes_bitexact_vs_oracle():
               "tlds": gpu_synth(Ny, Nz, lo, hi, seed=seed, coeff_mode="table")}
         hs["tlds"].set_tuning("ylds", 2)
         hs["tlds"].set_tuning("rows_per_wave", int(rs.choice([1, 2, 4])))
-        for k, v in (("gen_split", 1), ("fuse_plan", 0), ("gen_dense", 1)):
+        for k, v in (("gen_split", 1), ("fuse_plan", 0), ("gen_dense", 2)):
             hs["dense"].set_tuning(k, v)
         hs["coop2"].set_tuning("ycoop", 7)
         hs["coop2"].set_tuning("ycoop_order", int(rs.choice([0, 1, 4])))

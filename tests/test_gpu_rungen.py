@@ -13,10 +13,8 @@ pytestmark = pytest.mark.gpu
 FIELDS = ("u", "v", "w", "T", "rho")
 
 
-def force_run_form(monkeypatch):
-    # small planes otherwise take the fused-plan / split-wave K3 (no dense generation)
-    for k, v in (("DFAMD_GEN_DENSE", "2"), ("DFAMD_FUSE_PLAN", "0"), ("DFAMD_GEN_SPLIT", "1")):
-        monkeypatch.setenv(k, v)
+# small planes otherwise take the fused-plan / split-wave K3 (no run generation): applied after create
+RUN = dict(gen_dense=2, fuse_plan=0, gen_split=1)
 
 
 def check(hs, o, what):
@@ -32,11 +30,10 @@ def check(hs, o, what):
 
 @pytest.mark.parametrize("spec", [(131, 700, 2, 16), (57, 1100, 3, 90), (37, 129, 2, 10), (40, 133, 2, 8),
                                   (300, 260, 2, 24), (2, 1, 2, 2)])
-def test_run_generation_single_gpu_matches_oracle(monkeypatch, spec):
-    force_run_form(monkeypatch)
+def test_run_generation_single_gpu_matches_oracle(spec):
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=31)
     g = dfamd.DigitalFilter(plane="synthetic", Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=31,
-                            device=0, coeff_mode="table")
+                            device=0, coeff_mode="table", tuning=RUN)
     assert g.get_tuning("gen_dense") == 2
     check([g], o, "step0")
     flags = set()
@@ -49,13 +46,12 @@ def test_run_generation_single_gpu_matches_oracle(monkeypatch, spec):
 
 
 @pytest.mark.parametrize("world,Nz", [(2, 700), (3, 1100), (4, 1700), (8, 2048)])
-def test_run_generation_split_counting_strips_match_oracle(monkeypatch, world, Nz):
+def test_run_generation_split_counting_strips_match_oracle(world, Nz):
     # in-process strips count 1/world of the attempt blocks each and exchange group counts (device copies in
     # place of the all-gather); every strip recomputes the accept flags of the groups its pieces walk
-    force_run_form(monkeypatch)
     spec = dict(plane="synthetic", Ny=96, Nz=Nz, N_min=4, N_max=16, seed=8, device=0, coeff_mode="table")
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=96, Nz=Nz, N_min=4, N_max=16, seed=8)
-    hs = dfamd.create_group(world, **spec)
+    hs = dfamd.create_group(world, tuning=RUN, **spec)
     check(hs, o, "step0")
     for i in range(3):
         o.filter(1e-8)
@@ -63,14 +59,13 @@ def test_run_generation_split_counting_strips_match_oracle(monkeypatch, world, N
         check(hs, o, f"call {i}")
 
 
-def test_run_generation_switch_forms_mid_run(monkeypatch):
-    # gen_dense 0 / 1 / 2 switched between calls on one handle: the noise of every form is the same bits
-    force_run_form(monkeypatch)
+def test_run_generation_switch_forms_mid_run():
+    # gen_dense 0 / 2 switched between calls on one handle: the noise of every form is the same bits
     spec = (200, 300, 4, 24)
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=5)
     g = dfamd.DigitalFilter(plane="synthetic", Ny=spec[0], Nz=spec[1], N_min=spec[2], N_max=spec[3], seed=5,
-                            device=0, coeff_mode="table")
-    for i, form in enumerate((1, 2, 0, 2, 2, 1)):
+                            device=0, coeff_mode="table", tuning=RUN)
+    for i, form in enumerate((0, 2, 0, 2, 2, 0)):
         g.set_tuning("gen_dense", form)
         o.filter(1e-8)
         g.filter(1e-8)

@@ -144,18 +144,20 @@ def test_c_abi_rejects_bad_arguments():
     assert L.df_set_tuning(f._h, b"rows_per_wave", 2) == 0
     # launch-shape keys that rebalance device tile lists must not touch the absent device state
     # (a host-only handle never built its tap ranges)
-    for key in (b"ycoop_ovh", b"ycoop"):
+    for key in (b"ycoop_order", b"ycoop"):
         assert L.df_set_tuning(f._h, key, 7) == 0
     native = host()  # the reference's grid: long y chains, the row-pair plan
-    assert L.df_set_tuning(native._h, b"ycoop_ovh", 64) == 0
-    # round-3 keys: the dispatch order re-plans device tables only on handles that have them
-    for key, val in ((b"ycoop_order", 4), (b"ycoop_order", 0), (b"k3a_fast", 0), (b"ydepth", 0), (b"yunroll", 8),
-                     (b"halo_overlap", 0), (b"halo_overlap", -1), (b"gen_dense", 2), (b"fused_exchange", 0)):
+    # the dispatch order re-plans device tables only on handles that have them
+    for key, val in ((b"ycoop_order", 4), (b"ycoop_order", 0), (b"yunroll", 8), (b"halo_overlap", 0),
+                     (b"halo_overlap", -1), (b"gen_dense", 2), (b"gen_dense", 0), (b"fused_exchange", 0)):
         assert L.df_set_tuning(native._h, key, val) == 0, key
     assert L.df_set_tuning(native._h, b"ycoop_order", -1) == -1
-    # round 4: variants measured neutral or slower are gone from the library, not just off
+    assert L.df_set_tuning(native._h, b"gen_dense", 1) == -1  # round 5: Kc + K3a removed
+    # variants measured neutral or slower are gone from the library, not just off (round 4; round 5: the
+    # table y-pass's shared-kernel forms, K3a's destinations switch, the z unroll / store / balance knobs)
     for key in (b"ycoop_map", b"ypre", b"zocc", b"graph", b"count_grid", b"dense_g", b"gen_compact", b"nt_loads",
-                b"heavy_first", b"ylds_nw", b"ylds_ch"):
+                b"heavy_first", b"ylds_nw", b"ylds_ch", b"ydepth", b"ywindow", b"ydeep", b"k3a_fast", b"zunroll",
+                b"ycoop_ovh", b"znt_stores", b"ynt_stores", b"rng_nt_stores"):
         assert L.df_set_tuning(native._h, key, 1) == -1, key
         assert b"unknown tuning" in L.df_last_error()
     assert L.df_set_tuning(native._h, b"ycoop", 3) == -1
@@ -332,7 +334,7 @@ def test_alloc_registry_rejects_overlapping_ranges():
     # c3 (half-widths 4-64): table 4 rows per wave (ypass_table_kernel), no LDS staging, two generations per
     # hand-off, the run generation; packed 2 rows, one hand-off per call
     (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "table",
-     dict(rows_per_wave=4, ylds=0, handoff_batch=2, ycoop=0, gen_dense=2, ydepth=1)),
+     dict(rows_per_wave=4, ylds=0, handoff_batch=2, ycoop=0, gen_dense=2)),
     (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "packed",
      dict(rows_per_wave=2, ylds=0, ycoop=0, handoff_batch=1)),
     # c2: epochs of 2

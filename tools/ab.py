@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """In-process A/B timing of library variants on one GPU (guide §5.4 rule 24).
 
-    python3 tools/ab.py --a "DFAMD_GEN_DENSE=1" --b "DFAMD_GEN_DENSE=2" [--config c3] [--mode table]
+    python3 tools/ab.py --a "DFAMD_RNG_OVERLAP=1" --b "DFAMD_RNG_OVERLAP=0" [--config c3] [--mode table]
 
 Each variant is a separate handle created with its env knobs set; the handles
 run interleaved rounds of K calls and the per-phase hipEvent times are reported
 as median over rounds.
 
-    python3 tools/ab.py --tune-a rows_per_wave=4 --tune-b rows_per_wave=2,zunroll=4
+    python3 tools/ab.py --tune-a rows_per_wave=4 --tune-b rows_per_wave=2,yunroll=4
 
 --tune-* variants run on ONE handle (df_set_tuning between rounds), so both see
 the same allocations: separate handles differ by up to ~4% from page placement.

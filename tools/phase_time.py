@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
 """Per-phase device time of filter(dt) for one handle (timing experiments; not a test).
 
-    DFAMD_LIB=digital-filtering_amd/libdfamd_abl_noise.so python3 tools/phase_time.py --config c3
+    python3 tools/phase_time.py --config c3      (DFAMD_LIB=<another build of libdfamd.so> to time that one)
 
 Prints one JSON line: median over rounds of the hipEvent phase times (ms per call).
-With DFAMD_LIB pointing at a Makefile `variant` build the fields are wrong by design.
 """
 import argparse
 import json

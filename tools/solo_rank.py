@@ -19,13 +19,13 @@ p.add_argument("--calls", type=int, default=20)
 p.add_argument("--replicate", type=int, default=None)
 p.add_argument("--tune", default="", help="k=v,... df_set_tuning after create")
 a = p.parse_args()
-if a.replicate is not None:
-    os.environ["DFAMD_RNG_REPLICATE"] = str(a.replicate)
 import dfamd  # noqa: E402
 
 Ny, Nz = {"c4": (2048, 8192), "c5": (4096, 4096), "weak": (2048, 2048 * a.N)}[a.config]
 f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=4, N_max=64, seed=1, device=0, rank=a.rank,
                         world=a.N, coeff_mode=a.mode)
+if a.replicate is not None:
+    f.set_tuning("rng_replicate", a.replicate)
 for kv in filter(None, a.tune.split(":")):
     f.set_tuning(kv.split("=")[0], int(kv.split("=")[1]))
 for _ in range(a.calls):

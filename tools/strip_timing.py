@@ -32,7 +32,6 @@ p.add_argument("--env", default="", help="K=V:K=V... environment knobs set befor
 a = p.parse_args()
 for kv in filter(None, a.env.split(":")):
     os.environ[kv.split("=")[0]] = kv.split("=")[1]
-os.environ["DFAMD_RNG_REPLICATE"] = str(a.replicate)
 import dfamd  # noqa: E402
 
 for N in [int(x) for x in a.ns.split(",")]:
@@ -40,6 +39,7 @@ for N in [int(x) for x in a.ns.split(",")]:
     for rank in sorted({0, N // 2}):
         f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=4, N_max=64, seed=1, device=0,
                                 rank=rank, world=N, coeff_mode=a.mode)
+        f.set_tuning("rng_replicate", a.replicate)
         for kv in filter(None, a.tune.split(":")):
             f.set_tuning(kv.split("=")[0], int(kv.split("=")[1]))
         for _ in range(3):

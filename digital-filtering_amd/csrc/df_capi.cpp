@@ -75,6 +75,7 @@ struct CompDev {
     double *By = nullptr, *Bz = nullptr;
     long long *byoff = nullptr, *bzoff = nullptr;
     int *Ny_st = nullptr, *Nz_st = nullptr;     // tap range per (strip, row), [s*Ny + j]
+    int *Ny_st_g = nullptr;                     // the same over the strip widened by its ghost columns
     int *Ny_cell = nullptr, *Nz_cell = nullptr; // per-cell N of this strip (grid planes only)
     double *filt_old = nullptr, *fluc = nullptr, *filt = nullptr;
     long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
@@ -196,9 +197,22 @@ struct df_handle {
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
-    int yt_rows = 4;         // ypass_t64: rows per wave (1, 2, 4, 8)
+    int yt_rows = 2, yt_chunk = 8; // ypass_t64: rows per wave, noise rows per LDS chunk
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
+    // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
+    // Gl / Gr columns of its neighbours' (the widest z half-width, Nzp), straight into its z-halo, so the z-pass
+    // needs no exchange; the RNG generates those columns' r_ys too. ghost_cap: the layout and tables exist
+    // (ry pitch Pzy holds Wext columns); ghost: in use.
+    int ghost_cap = 0, ghost = 0;
+    int Gl = 0, Gr = 0, Wext = 0, nstrips_g = 0, Pzy = 0;
+    int *ylist_g = nullptr;  // ypass_t64 order over the widened strip
+    int ylist_g_n = 0, ylist_g_nrb = 0, ylist_g_ncol = 0, ylist_g_cap = 0;
+    struct RunTables {
+        const ChunkDest *chunk_dest[2] = {};
+        const RunPiece *pieces[2] = {};
+        int npieces[2] = {};
+    } run_tab[2]; // run generation tables without (0) and with (1) the ghost columns
     bool dense_ready = false; // the run generation's chunk tables are built (alloc_dense)
     RngGeom geom{};
     // halo
@@ -322,7 +336,7 @@ SweepArgs sweep_args(df_handle *h)
     }
     a.Ny = h->Ny;
     a.Nz_loc = h->Nz_loc;
-    a.Pz = h->Pz;
+    a.Pz = h->Pzy; // ry pitch (the y-pass's noise); the z-pass reads rz only
     a.nstrips = h->nstrips;
     a.zs_lo = 0;
     a.zs_n = a.zs_gap_at = h->nstrips;
@@ -358,6 +372,12 @@ SweepArgs sweep_args(df_handle *h)
     a.ylist_nrb = h->ylist_nrb;
     a.ylist_ncol = h->ylist_ncol;
     a.ylist_R = h->yt_rows;
+    a.ylist_C = h->yt_chunk;
+    for (int c = 0; c < 3; ++c) {
+        a.yout[c] = h->c[c].Nzp;
+        a.ylo[c] = 0;
+        a.yhi[c] = h->Nz_loc;
+    }
     a.zsplit = h->zsplit;
     a.zunroll = h->zunroll;
     a.nt_stores = h->nt_stores;
@@ -672,6 +692,17 @@ int fused_gen_begin(df_handle *h)
     if (h->pend_g.gen_dense != 2) return DF_OK; // cannot happen with fused_active; the plain path then runs
     HIP_OR(hipEventRecord(h->ev_counted, rs), DF_EHIP);
     h->gen_pending = true;
+    if (h->ghost) { // no halo group to ride in: the records' all-gather follows the counts on the RNG stream, so
+                    // the sweep stream never waits on a collective (the sweeps of calls k, k + 1 run beside it)
+        if (h->comm && !h->solo_strip) {
+            const size_t ngc = (size_t)h->pend_g.xstride;
+            NCCL_OR(ncclAllGather(h->pend_g.xbuf + (size_t)h->rank * ngc, h->pend_g.xbuf, ngc, ncclUint8, h->rng_comm, rs));
+            HIP_OR(hipEventRecord(h->ev_halo, rs), DF_EHIP);
+        } else { // solo strip: the exchange's stand-in (and its held time) on the RNG stream
+            if (h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, rs), DF_EHIP);
+            HIP_OR(hipEventRecord(h->ev_xchg, rs), DF_EHIP);
+        }
+    }
     return DF_OK;
 }
 
@@ -694,6 +725,20 @@ int phase_ypass(df_handle *h, int comps_mask)
 {
     SweepArgs a = sweep_args(h);
     a.comps_mask = comps_mask;
+    if (h->ghost) { // the strip widened by its ghost columns; each component keeps the Nzp columns its halo holds
+        a.Nz_loc = h->Wext;
+        a.nstrips = h->nstrips_g;
+        a.ylist = h->ylist_g;
+        a.ylist_n = h->ylist_g_n;
+        a.ylist_nrb = h->ylist_g_nrb;
+        a.ylist_ncol = h->ylist_g_ncol;
+        for (int c = 0; c < 3; ++c) {
+            a.Ny_st[c] = h->c[c].Ny_st_g;
+            a.yout[c] = h->c[c].Nzp - h->Gl;
+            a.ylo[c] = h->Gl - h->c[c].Nzp > 0 ? h->Gl - h->c[c].Nzp : 0;
+            a.yhi[c] = std::min(h->Wext, h->Gl + h->Nz_loc + (h->Gr ? h->c[c].Nzp : 0));
+        }
+    }
     HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, h->stream), DF_EHIP);
     return DF_OK;
 }
@@ -763,6 +808,7 @@ int halo_sendrecv(df_handle *h, hipStream_t st)
 int phase_halo_rccl(df_handle *h)
 {
     if (h->world == 1) return h->halo_loopback && h->comm ? halo_loopback(h) : DF_OK;
+    if (h->ghost) return DF_OK; // the y-pass filled the z-halo itself
     if (h->solo_strip) { // timing only: the pack, no exchange (or a hold of DFAMD_SOLO_XCHG_US in its place)
         int rc = phase_halo_pack(h);
         if (!rc && h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, h->stream), DF_EHIP);
@@ -802,7 +848,7 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
     int lo = 0, hi = 0, rc;
     const bool peer = h->comm && !h->solo_strip; // DFAMD_SOLO_STRIP (timing only): the same streams, no exchange
     const bool ov = h->halo_overlap > 0 || (h->halo_overlap < 0 && h->coeff_mode == DF_COEFF_PACKED);
-    if (h->world == 1 || !(peer || h->solo_strip) || !ov || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
+    if (h->world == 1 || h->ghost || !(peer || h->solo_strip) || !ov || !h->comm_stream || !halo_interior(h, &lo, &hi)) {
         if ((rc = phase_halo_rccl(h))) return rc;
         ev_record(h, 2);
         return phase_zpass(h, corr, sra, dt);
@@ -1004,17 +1050,19 @@ int upload_ycoop2_perm(df_handle *h, int c)
 
 // Dispatch order of ypass_t64_kernel (ylds 3): blocks of 4 * yt_rows rows x 64 columns of every component, the
 // largest union of noise rows (a block's chunk count, so its time) first; ties keep component, tile, row order.
-int build_ylist(df_handle *h)
+// ghost: over the strip widened by its ghost columns (row-uniform N: every column of a row has the row's N).
+int build_ylist(df_handle *h, bool ghost)
 {
     const int Ny = h->Ny, RB = 4 * h->yt_rows;
-    const int ncol = (h->Nz_loc + 63) / 64, nrb = (Ny + RB - 1) / RB;
+    const int W = ghost ? h->Wext : h->Nz_loc;
+    const int ncol = (W + 63) / 64, nrb = (Ny + RB - 1) / RB;
     const int n = 3 * ncol * nrb;
-    if (n > h->ylist_cap) return fail(DF_EINVAL, "ypass_t64 tile list larger than its allocation");
+    if (n > (ghost ? h->ylist_g_cap : h->ylist_cap)) return fail(DF_EINVAL, "ypass_t64 tile list larger than its allocation");
     std::vector<std::pair<int, int>> cost(n); // (-noise rows, tile)
     for (int c = 0; c < 3; ++c)
         for (int ct = 0; ct < ncol; ++ct)
             for (int rb = 0; rb < nrb; ++rb) {
-                const int *nst = h->y_nst[c].data() + (size_t)(ct >> 1) * Ny;
+                const int *nst = ghost ? h->setup.comp[c].Ny_row.data() : h->y_nst[c].data() + (size_t)(ct >> 1) * Ny;
                 int lo = 1 << 30, hi = -(1 << 30);
                 for (int j = rb * RB; j < std::min(Ny, rb * RB + RB); ++j) {
                     lo = std::min(lo, j - nst[j]);
@@ -1026,10 +1074,17 @@ int build_ylist(df_handle *h)
     std::stable_sort(cost.begin(), cost.end(), [](const auto &p, const auto &q) { return p.first < q.first; });
     std::vector<int> order(n);
     for (int i = 0; i < n; ++i) order[i] = cost[i].second;
-    h->ylist_n = n;
-    h->ylist_nrb = nrb;
-    h->ylist_ncol = ncol;
-    return upload(h, h->ylist, order.data(), order.size());
+    (ghost ? h->ylist_g_n : h->ylist_n) = n;
+    (ghost ? h->ylist_g_nrb : h->ylist_nrb) = nrb;
+    (ghost ? h->ylist_g_ncol : h->ylist_ncol) = ncol;
+    return upload(h, ghost ? h->ylist_g : h->ylist, order.data(), order.size());
+}
+
+int build_ylists(df_handle *h)
+{
+    int rc = h->ylist ? build_ylist(h, false) : DF_OK;
+    if (!rc && h->ylist_g) rc = build_ylist(h, true);
+    return rc;
 }
 
 // This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
@@ -1116,6 +1171,21 @@ int plan_strips(df_handle *h)
         }
     }
 
+    // Ghost columns (table-mode z-strips, row-uniform N): the widest z half-width of the plane's components
+    // (Nzp, which the z-halo holds) on each side that has a neighbour. The ry pitch Pzy holds the widened strip.
+    h->Pzy = h->Pz;
+    if (h->coeff_mode == DF_COEFF_TABLE && h->world > 1 && !s.per_cell) {
+        int G = 0;
+        for (int c = 0; c < 3; ++c) G = std::max(G, h->c[c].Nzp);
+        G = (G + 1) / 2 * 2; // even: the y-pass's 16-B pairs stay aligned in rz
+        h->ghost_cap = 1;
+        h->Gl = h->rank > 0 ? G : 0;
+        h->Gr = h->rank < h->world - 1 ? G : 0;
+        h->Wext = h->Nz_loc + h->Gl + h->Gr;
+        h->nstrips_g = (h->Wext + kStrip - 1) / kStrip;
+        h->Pzy = std::max(h->Pz, h->nstrips_g * kStrip);
+    }
+
     // Write windows (SweepArgs::ywin_T): on planes whose sweeps stream >= 2 GB of packed coefficients per
     // pass the waves hold their stores for a chip-wide window of 2.56 us every 41 us; c3 -5.1% per call,
     // c5 -3.1% (profiles/r1/probe/win_*.json). Smaller planes (c2: +4.7%) and the VALU-bound table mode
@@ -1169,9 +1239,11 @@ int plan_rng(df_handle *h)
         g.next_plus3 = j3.mult * next.plus + j3.plus - next.mult * j3.plus;
     }
     g.Nz_g = s.Nz;
-    g.Pz = h->Pz;
+    g.Pz = h->Pzy;
     g.z0 = h->z0;
     g.z1 = h->z1;
+    g.yz0 = h->z0; // ghost columns off (select_ghost switches)
+    g.yz1 = h->z1;
     g.is_first = h->rank == 0;
     g.is_last = h->rank == h->world - 1;
     {
@@ -1296,7 +1368,7 @@ int alloc_components(df_handle *h)
         CompDev &d = h->c[c];
         const ComponentSetup &F = s.comp[c];
         for (int set = 0; set < h->nsets; ++set) {
-            if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp) * h->Pz))) return rc;
+            if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp) * h->Pzy))) return rc;
             if ((rc = dalloc_t(h, &d.rz[set], (size_t)Ny * d.rz_pitch))) return rc;
         }
         if ((rc = dalloc_t(h, &d.filt_old, n_loc))) return rc;
@@ -1324,10 +1396,22 @@ int alloc_components(df_handle *h)
         if ((rc = dalloc_t(h, &d.Nz_st, Nst[1].size()))) return rc;
         if ((rc = upload(h, d.Ny_st, Nst[0].data(), Nst[0].size()))) return rc;
         if ((rc = upload(h, d.Nz_st, Nst[1].data(), Nst[1].size()))) return rc;
+        if (h->ghost_cap) { // the widened strip's tap ranges: row-uniform, the same for each of its 128-column strips
+            std::vector<int> ng((size_t)h->nstrips_g * Ny);
+            for (int st = 0; st < h->nstrips_g; ++st)
+                for (int j = 0; j < Ny; ++j) ng[(size_t)st * Ny + j] = F.Ny_row[j];
+            if ((rc = dalloc_t(h, &d.Ny_st_g, ng.size()))) return rc;
+            if ((rc = upload(h, d.Ny_st_g, ng.data(), ng.size()))) return rc;
+        }
         if (c == 2 && h->coeff_mode == DF_COEFF_TABLE && !s.per_cell) { // ypass_t64's list, sized for 1 row per wave
             h->ylist_cap = 3 * ((h->Nz_loc + 63) / 64) * ((Ny + 3) / 4);
             if ((rc = dalloc_t(h, &h->ylist, h->ylist_cap))) return rc;
-            if ((rc = build_ylist(h))) return rc;
+            if ((rc = build_ylist(h, false))) return rc;
+            if (h->ghost_cap) {
+                h->ylist_g_cap = 3 * ((h->Wext + 63) / 64) * ((Ny + 3) / 4);
+                if ((rc = dalloc_t(h, &h->ylist_g, h->ylist_g_cap))) return rc;
+                if ((rc = build_ylist(h, true))) return rc;
+            }
         }
         if (s.per_cell) {
             std::vector<int> nc[2];
@@ -1480,9 +1564,11 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
 // 64-rank chunks whose pairs (positions f + 2r, f + 2r + 1) store something on this GPU - the same
 // columns as stream_dest: r_ys columns [z0, z1), r_zs pads on the plane's first/last strip - plus the
 // chunk of the call's last rank A - 1 (it sets the stream state); their fast destinations and the pieces.
-int alloc_dense(df_handle *h)
+int build_run_tables(df_handle *h, int yz0, int yz1, df_handle::RunTables &out)
 {
-    const RngGeom &g = h->geom;
+    RngGeom g = h->geom;
+    g.yz0 = yz0;
+    g.yz1 = yz1;
     const uint64_t A0 = (g.Q + 1) / 2; // A for f = 0 (f = 1: A0 or A0 - 1)
     const uint64_t nch = (A0 + 63) / 64;
     if (nch >= (1ull << 31)) return fail(DF_EINVAL, "plane too large for the dense generation tables");
@@ -1501,9 +1587,9 @@ int alloc_dense(df_handle *h)
             const uint64_t base = g.seg[sidx], W = g.width[sidx], rows = g.rows[sidx];
             const int cmp = sidx >> 1;
             if ((sidx & 1) == 0) { // r_ys: this strip's columns of every row
-                if (g.z0 == 0 && (uint64_t)g.z1 == W) mark(base, base + rows * W);
+                if (g.yz0 == 0 && (uint64_t)g.yz1 == W) mark(base, base + rows * W);
                 else
-                    for (uint64_t r = 0; r < rows; ++r) mark(base + r * W + g.z0, base + r * W + g.z1);
+                    for (uint64_t r = 0; r < rows; ++r) mark(base + r * W + g.yz0, base + r * W + g.yz1);
             } else { // r_zs: the raw-noise pads (df.cpp:343-348) on the plane's edge strips
                 const uint64_t nzp = (uint64_t)g.Nzp[cmp];
                 for (uint64_t r = 0; r < rows; ++r) {
@@ -1524,8 +1610,8 @@ int alloc_dense(df_handle *h)
     auto dest_of = [&g](int su, uint64_t row, uint64_t col, long long &off) { // host mirror of stream_dest
         const int cmp = su >> 1;
         if ((su & 1) == 0) {
-            if (col < (uint64_t)g.z0 || col >= (uint64_t)g.z1) return false;
-            off = (long long)(row * (uint64_t)g.Pz + (col - (uint64_t)g.z0));
+            if (col < (uint64_t)g.yz0 || col >= (uint64_t)g.yz1) return false;
+            off = (long long)(row * (uint64_t)g.Pz + (col - (uint64_t)g.yz0));
             return true;
         }
         long long lc;
@@ -1596,7 +1682,7 @@ int alloc_dense(df_handle *h)
         ChunkDest *dd = nullptr;
         if ((rc = dalloc_t(h, &dd, dest[f].size()))) return rc;
         if ((rc = upload(h, dd, dest[f].data(), dest[f].size()))) return rc;
-        h->geom.chunk_dest[f] = dd;
+        out.chunk_dest[f] = dd;
     }
     // Run generation (gen_dense 2): the list cut into pieces of consecutive chunks, at most kRunPiece each and
     // of near-equal length within a run (a 9-chunk row segment of a strip is one piece, not 8 + 1)
@@ -1619,9 +1705,32 @@ int alloc_dense(df_handle *h)
         RunPiece *dp = nullptr;
         if ((rc = dalloc_t(h, &dp, std::max<size_t>(1, pcs.size())))) return rc;
         if (!pcs.empty() && (rc = upload(h, dp, pcs.data(), pcs.size()))) return rc;
-        h->geom.pieces[f] = dp;
-        h->geom.npieces[f] = (int)pcs.size();
+        out.pieces[f] = dp;
+        out.npieces[f] = (int)pcs.size();
     }
+    return DF_OK;
+}
+
+// The r_ys columns the RNG stores and the run tables for the ghost mode in use.
+void apply_ghost_geom(df_handle *h)
+{
+    const int m = h->ghost ? 1 : 0;
+    h->geom.yz0 = h->ghost ? h->z0 - h->Gl : h->z0;
+    h->geom.yz1 = h->ghost ? h->z1 + h->Gr : h->z1;
+    if (!h->dense_ready && !h->run_tab[0].pieces[0]) return; // run tables not built (yet)
+    for (int f = 0; f < 2; ++f) {
+        h->geom.chunk_dest[f] = h->run_tab[m].chunk_dest[f];
+        h->geom.pieces[f] = h->run_tab[m].pieces[f];
+        h->geom.npieces[f] = h->run_tab[m].npieces[f];
+    }
+}
+
+int alloc_dense(df_handle *h)
+{
+    int rc = build_run_tables(h, h->z0, h->z1, h->run_tab[0]);
+    if (!rc && h->ghost_cap) rc = build_run_tables(h, h->z0 - h->Gl, h->z1 + h->Gr, h->run_tab[1]);
+    if (rc) return rc;
+    apply_ghost_geom(h);
     h->dense_ready = true;
     return DF_OK;
 }
@@ -1769,16 +1878,20 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         if ((rc = check_rng_error(h))) return rc;
         if ((rc = consume_gen(h))) return rc;
         if ((rc = phase_ypass(h, 7))) return rc;
-        if ((rc = phase_halo_pack(h))) return rc;
+        if (!h->ghost && (rc = phase_halo_pack(h))) return rc;
     }
-    for (int r = 0; r < n; ++r) HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
+    const bool ghost = hs[0]->ghost != 0;
+    for (int r = 0; r < n; ++r)
+        if (hs[r]->ghost != hs[0]->ghost) return fail(DF_EINVAL, "halo_ghost differs between the strips of a group");
+    if (!ghost)
+        for (int r = 0; r < n; ++r) HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
     for (int r = 0; r < n; ++r) {
         df_handle *h = hs[r];
         HIP_OR(hipSetDevice(h->device), DF_EHIP);
         const size_t bytes = h->halo_elems * sizeof(double);
-        if (r > 0) HIP_OR(hipMemcpyAsync(h->recv_l, hs[r - 1]->send_r, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
-        if (r < n - 1) HIP_OR(hipMemcpyAsync(h->recv_r, hs[r + 1]->send_l, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
-        if ((rc = phase_halo_unpack(h))) return rc;
+        if (!ghost && r > 0) HIP_OR(hipMemcpyAsync(h->recv_l, hs[r - 1]->send_r, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
+        if (!ghost && r < n - 1) HIP_OR(hipMemcpyAsync(h->recv_r, hs[r + 1]->send_l, bytes, hipMemcpyDefault, h->stream), DF_EHIP);
+        if (!ghost && (rc = phase_halo_unpack(h))) return rc;
         if ((rc = phase_zpass(h, corr_sra, corr_sra, dt))) return rc;
         if ((rc = prefetch_gen(h))) return rc;
     }
@@ -2241,11 +2354,12 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"zsplit", h->zsplit},
+        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"zsplit", h->zsplit},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
-        {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap}};
+        {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap},
+        {"halo_ghost", h->ghost}};
     for (const auto &kv : keys)
         if (k == kv.first) {
             *value = kv.second;
@@ -2273,11 +2387,41 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
-    } else if (k == "yt_rows") {
-        if (value != 1 && value != 2 && value != 4 && value != 8) return fail(DF_EINVAL, "yt_rows must be 1, 2, 4 or 8");
-        h->yt_rows = value;
-        if (h->ylist)
-            if (int rc = build_ylist(h)) return rc;
+    } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 2 x 8, 2 x 16, 4 x 8
+        const int R = k == "yt_rows" ? value : h->yt_rows, C = k == "yt_chunk" ? value : h->yt_chunk;
+        const int Cd = R == 1 ? 16 : 8; // a row count alone takes its default chunk
+        const int Cu = k == "yt_rows" && !(R == 2 && (C == 8 || C == 16)) ? Cd : C;
+        if (!((R == 1 && Cu == 16) || (R == 2 && (Cu == 8 || Cu == 16)) || (R == 4 && Cu == 8)))
+            return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 2 x 8, 2 x 16 or 4 x 8");
+        if (h->device >= 0)
+            if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
+        h->yt_rows = R;
+        h->yt_chunk = Cu;
+        if (int rc = build_ylists(h)) return rc;
+    }
+    else if (k == "halo_ghost") { // the same on every rank of a plane (it decides whether a halo exchange runs)
+        if (value && !h->ghost_cap)
+            return fail(DF_EINVAL, "halo_ghost needs a table-mode z-strip handle with row-uniform half-widths");
+        if ((value != 0) != (h->ghost != 0)) {
+            std::vector<df_handle *> mem = h->group ? *h->group : std::vector<df_handle *>{h};
+            if (h->device >= 0)
+                for (df_handle *m : mem) // queued generations and sweeps keep the layout they had
+                    if (int rc = sync_all(m)) return rc;
+            h->ghost = value != 0;
+            apply_ghost_geom(h);
+            // prefetched noise has the other layout: redo it (an in-process group generates for every strip at
+            // once, so once all its strips agree)
+            bool agree = true;
+            for (df_handle *m : mem) agree = agree && m->ghost == h->ghost;
+            if (h->device >= 0 && agree && h->gen_launched > h->gen_used) {
+                if (!h->group) {
+                    if (int rc = restart_pipeline(h, h->hb)) return rc;
+                } else {
+                    for (df_handle *m : mem) m->gen_launched = m->gen_used; // hb 1: one generation each, redone
+                    if (int rc = launch_gen(h)) return rc;
+                }
+            }
+        }
     }
     else if (k == "halo_overlap") {
         if (h->device >= 0)
@@ -2429,7 +2573,8 @@ int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n)
     const int rows = dir ? h->Ny : h->Ny + 2 * d.Nyp;
     if (n < (long long)width * rows) return fail(DF_EINVAL, "output too small");
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
-    HIP_OR(hipMemcpy2DAsync(out, (size_t)width * 8, dir ? d.rz[h->cur] : d.ry[h->cur], (size_t)(dir ? d.rz_pitch : h->Pz) * 8,
+    const double *src = dir ? d.rz[h->cur] : d.ry[h->cur] + (h->ghost ? h->Gl : 0); // ghost: the strip's own columns
+    HIP_OR(hipMemcpy2DAsync(out, (size_t)width * 8, src, (size_t)(dir ? d.rz_pitch : h->Pzy) * 8,
                             (size_t)width * 8, rows, hipMemcpyDeviceToHost, h->stream),
            DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
@@ -2470,10 +2615,11 @@ int df_comm_info(df_handle *h, df_comm_stats *out)
         NCCL_OR(ncclCommUserRank(h->comm, &out->rccl_rank));
     }
     const bool split = h->world > 1 || h->halo_loopback;
-    out->halo_peers = h->world > 1 ? (h->rank > 0) + (h->rank < h->world - 1) : (h->halo_loopback ? 2 : 0);
+    out->halo_peers = h->ghost ? 0 : h->world > 1 ? (h->rank > 0) + (h->rank < h->world - 1) : (h->halo_loopback ? 2 : 0);
     out->halo_bytes_sent = split ? (long long)out->halo_peers * (long long)h->halo_elems * 8 : 0;
     // 2: the records ride in the halo's ncclGroup (one grouped RCCL operation per call); 1: an all-gather of their own
-    out->rng_collective = h->split_count && h->rng_comm ? (fused_active(h) ? 2 : 1) : 0;
+    // (halo_ghost: no halo, the records travel alone on the RNG stream: 1)
+    out->rng_collective = h->split_count && h->rng_comm ? (fused_active(h) && !h->ghost ? 2 : 1) : 0;
     const long long others = (long long)h->rng_chunk * (h->world - 1);
     long long rec = 0, lo = 0, to = 0;
     record_layout(h->rng_chunk, &rec, &lo, &to);

@@ -291,8 +291,8 @@ template <class G> __device__ __forceinline__ double *stream_dest(const G &g, St
     const int c = s.sidx >> 1;
     const int col = (int)s.col;
     if ((s.sidx & 1) == 0) { // r_ys: Nz_g columns per row
-        if (col < g.z0 || col >= g.z1) return nullptr;
-        return g.ry[c] + (size_t)s.row * g.Pz + (col - g.z0);
+        if (col < g.yz0 || col >= g.yz1) return nullptr;
+        return g.ry[c] + (size_t)s.row * g.Pz + (col - g.yz0);
     }
     int lc;
     if (col < g.Nzp[c]) {
@@ -330,7 +330,7 @@ template <class G> __device__ bool range_needed(const G &g, uint64_t q0, uint64_
         const uint32_t a = (uint32_t)(lo - g.seg[sidx]), b = (uint32_t)(hi - g.seg[sidx]);
         const uint32_t W = g.width[sidx];
         if ((sidx & 1) == 0) {
-            if (span_hits_cols(a, b, W, (uint32_t)g.z0, (uint32_t)g.z1)) return true;
+            if (span_hits_cols(a, b, W, (uint32_t)g.yz0, (uint32_t)g.yz1)) return true;
         } else {
             const uint32_t nzp = (uint32_t)g.Nzp[sidx >> 1];
             if (g.is_first && span_hits_cols(a, b, W, 0, nzp)) return true;
@@ -440,10 +440,10 @@ __device__ __forceinline__ WaveDest wave_dest(const RngGeom &g, uint64_t q_lo, u
     w.pitch = odd ? (size_t)sel(g.rz_pitch, cmp) : (size_t)g.Pz;
     w.row = P.row;
     w.col = P.col;
-    w.lo1 = odd ? 0u : (uint32_t)g.z0;
-    w.hi1 = odd ? (g.is_first ? nzp : 0u) : (uint32_t)g.z1;
+    w.lo1 = odd ? 0u : (uint32_t)g.yz0;
+    w.hi1 = odd ? (g.is_first ? nzp : 0u) : (uint32_t)g.yz1;
     w.lo2 = odd && g.is_last ? nzp + (uint32_t)g.Nz_g : w.W;
-    w.o1 = odd ? 0 : -g.z0;
+    w.o1 = odd ? 0 : -g.yz0;
     w.o2 = -g.z0;
     return w;
 }
@@ -1487,14 +1487,16 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
     for (; t <= bh; ++t) body_n(t, noise(t));
     for (; t <= thi; ++t) predicated(t);
     write_window(a.ywin_T, a.ywin_W);
+    if (col < a.ylo[c]) return; // ylo even: the lane's pair is wholly in or out
+    const int yhi = a.yhi[c];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (r < nr) {
-            double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.Nzp[c] + col;
-            if (col + 1 < a.Nz_loc) {
+            double *o = a.rz[c] + (size_t)(j0 + r) * a.rz_pitch[c] + a.yout[c] + col;
+            if (col + 1 < yhi) {
                 if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
                 else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
-            } else if (col < a.Nz_loc) o[0] = acc0[r];
+            } else if (col < yhi) o[0] = acc0[r];
         }
     }
 }
@@ -1761,14 +1763,16 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
             if (i + 2 < nch) step(ic_t<2 % PD>{}, i + 2);
     }
     write_window(a.ywin_T, a.ywin_W);
+    if (col < a.ylo[c]) return; // ylo even: the lane's pair is wholly in or out
+    const int yhi = a.yhi[c];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (jw + r >= Ny) continue;
-        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.Nzp[c] + col;
-        if (col + 1 < a.Nz_loc) {
+        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.yout[c] + col;
+        if (col + 1 < yhi) {
             if (a.ynt_stores) __builtin_nontemporal_store(dvec2{acc0[r], acc1[r]}, reinterpret_cast<dvec2 *>(o));
             else *reinterpret_cast<double2 *>(o) = make_double2(acc0[r], acc1[r]);
-        } else if (col < a.Nz_loc) o[0] = acc0[r];
+        } else if (col < yhi) o[0] = acc0[r];
     }
 }
 
@@ -1776,17 +1780,24 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 // for planes whose y-pass is a few hundred thousand cells of chains up to ~425 taps (the reference's own grid:
 // 510 x 400, N_y 14-212). One cell per lane, so a block covers a 64-column tile (the grid's 400 columns are 7
 // tiles with one 16-column tail instead of 4 strips with a 16-column tail that idled a quarter of the waves),
-// and R rows per wave, so each noise value read from LDS serves R products (R = 1 made the LDS array, not the
-// FP64 pipe, the limit). Blocks run in the host's order (SweepArgs::ylist): heaviest union of noise rows
-// first, components and tiles interleaved, so the widest stencils (N_y 206-212 around j = 160-200) start
-// first instead of wherever their rows fall. Each row adds its taps in the order i = -N..N (noise rows
-// ascending) with df.cpp:373-375's products: bit-identical to every other form.
+// and R rows per wave, so each noise value read from LDS serves R products (R = 1 makes the LDS array, not the
+// FP64 pipe, the limit: profiles/r5). Blocks run in the host's order (SweepArgs::ylist): heaviest union of
+// noise rows first, components and tiles interleaved, so the widest stencils (N_y 206-212 around j = 160-200)
+// start first instead of wherever their rows fall.
+// Waits: scalar loads return out of order, so while one is in flight every LDS wait is a full lgkmcnt(0). A
+// chunk's R x C coefficients (uniform: one scalar window per row) are therefore loaded before the chunk's
+// barrier, whose wait they share, and the chunk's sums then wait on LDS reads alone. The noise loads of the
+// chunks in flight go to clamped rows instead of being predicated, so their vmcnt waits are counted, not zero.
+// Each row adds its taps in the order i = -N..N (noise rows ascending) with df.cpp:373-375's products:
+// bit-identical to every other form.
 template <int R, int NW, int C, int PD>
 __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 {
-    constexpr int LW = C / NW; // chunk rows each wave loads
-    static_assert(C % NW == 0, "chunk rows split evenly over the waves");
-    __shared__ double nbuf[2][C][64];
+    constexpr int LP = C / (2 * NW); // pairs of chunk rows each wave loads
+    static_assert(C % (2 * NW) == 0, "chunk row pairs split evenly over the waves");
+    // noise rows 2p, 2p + 1 of a chunk side by side for each lane: one ds_read_b128 (4 LDS cycles for 1 KiB)
+    // fetches two rows, where the compiler's ds_read2st64_b64 of two separate rows takes 8
+    __shared__ dvec2 nbuf[2][C / 2][64];
     const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
     const int tile = a.ylist[blockIdx.x];
     const int nrb = a.ylist_nrb, ncol = a.ylist_ncol;
@@ -1817,62 +1828,79 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     }
     const int col = ct * 64 + lane; // < Pz: a padding column is loaded and summed but never stored
     const double *np = a.ry[c] + (size_t)a.Nyp[c] * a.Pz + col; // noise row m at np + m * Pz
-    double pre[PD][LW];
+    dvec2 pre[PD][LP]; // wave w loads row pairs w + NW k of the chunk
     auto gload = [&](auto K, int u0) {
         constexpr int k0 = decltype(K)::value;
 #pragma unroll
-        for (int k = 0; k < LW; ++k) {
-            const int m = u0 + w + NW * k; // wave-uniform
-            pre[k0][k] = m <= mhi ? np[(ptrdiff_t)m * a.Pz] : 0.0;
+        for (int k = 0; k < LP; ++k) {
+            const int m = u0 + 2 * (w + NW * k);
+            pre[k0][k] = dvec2{np[(ptrdiff_t)min(m, mhi) * a.Pz], np[(ptrdiff_t)min(m + 1, mhi) * a.Pz]};
         }
     };
     auto lstore = [&](auto K, int buf) {
         constexpr int k0 = decltype(K)::value;
 #pragma unroll
-        for (int k = 0; k < LW; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
+        for (int k = 0; k < LP; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
+    };
+    auto is_full = [&](int u0) { // every row of the wave takes all C noise rows of the chunk
+        bool f = u0 + C - 1 <= mhi;
+#pragma unroll
+        for (int r = 0; r < R; ++r) f = f && lo[r] <= u0 && hi[r] >= u0 + C - 1;
+        return f;
+    };
+    double cw[R][C]; // a full chunk's coefficients (uniform)
+    auto cload = [&](int u0) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int q = 0; q < C; ++q) cw[r][q] = tb[r][u0 - lo[r] + q];
     };
     double acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0;
-    auto compute = [&](int u0, int buf) {
-        const int mb = min(u0 + C - 1, mhi);
-        bool full = mb == u0 + C - 1, any = false;
+    auto compute = [&](int u0, int buf, bool full) {
+        if (full) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            full = full && lo[r] <= u0 && hi[r] >= mb;
-            any = any || (lo[r] <= mb && hi[r] >= u0);
+            for (int p = 0; p < C / 2; ++p) {
+                const dvec2 n = nbuf[buf][p][lane];
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p] * n.x;
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p + 1] * n.y;
+            }
+            return;
         }
-        if (full) { // every row of the wave takes all C noise rows of the chunk
-            const double *cb[R];
+        const int mb = min(u0 + C - 1, mhi);
+        bool any = false;
 #pragma unroll
-            for (int r = 0; r < R; ++r) cb[r] = tb[r] + (u0 - lo[r]);
+        for (int r = 0; r < R; ++r) any = any || (lo[r] <= mb && hi[r] >= u0);
+        if (!any) return;
+        for (int m = u0; m <= mb; ++m) {
+            const dvec2 n2 = nbuf[buf][(m - u0) >> 1][lane];
+            const double n = ((m - u0) & 1) ? n2.y : n2.x;
 #pragma unroll
-            for (int q = 0; q < C; ++q) {
-                const double n = nbuf[buf][q][lane];
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] += cb[r][q] * n;
-            }
-        } else if (any) {
-            for (int m = u0; m <= mb; ++m) {
-                const double n = nbuf[buf][m - u0][lane];
-#pragma unroll
-                for (int r = 0; r < R; ++r)
-                    if (m >= lo[r] && m <= hi[r]) acc[r] += tb[r][m - lo[r]] * n; // wave-uniform
-            }
+            for (int r = 0; r < R; ++r)
+                if (m >= lo[r] && m <= hi[r]) acc[r] += tb[r][m - lo[r]] * n; // wave-uniform
         }
     };
     // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
-    // ypass_tlds_kernel)
+    // ypass_tlds_kernel); its coefficients (full chunks) loaded before the barrier that precedes it
     const int nch = (mhi - mlo) / C + 1;
     gload(ic_t<0>{}, mlo);
     if constexpr (PD > 1) gload(ic_t<1 % PD>{}, mlo + C);
     lstore(ic_t<0>{}, 0);
+    bool full = is_full(mlo);
+    if (full) cload(mlo);
     __syncthreads();
     auto step = [&](auto K, int i) {
         constexpr int k = decltype(K)::value;
         if (i + PD < nch) gload(K, mlo + (i + PD) * C); // block-uniform
-        compute(mlo + i * C, i & 1);
-        if (i + 1 < nch) lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+        compute(mlo + i * C, i & 1, full);
+        if (i + 1 < nch) {
+            lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+            full = is_full(mlo + (i + 1) * C);
+            if (full) cload(mlo + (i + 1) * C);
+        }
         __syncthreads();
     };
     for (int i = 0; i < nch; i += PD) {
@@ -1880,11 +1908,11 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         if constexpr (PD > 1)
             if (i + 1 < nch) step(ic_t<1 % PD>{}, i + 1);
     }
-    if (col >= a.Nz_loc) return;
+    if (col < a.ylo[c] || col >= a.yhi[c]) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (jw + r >= Ny) continue;
-        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.Nzp[c] + col;
+        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.yout[c] + col;
         if (a.ynt_stores) __builtin_nontemporal_store(acc[r], o);
         else *o = acc[r];
     }
@@ -1895,11 +1923,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     if constexpr (TABLE) {
         if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
             const dim3 grid((unsigned)a.ylist_n);
-            switch (a.ylist_R) {
-            case 1: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-            case 2: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-            case 8: hipLaunchKernelGGL((ypass_t64_kernel<8, 4, 16, 1>), grid, dim3(256), 0, st, a); break;
-            default: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            // R x C coefficients of a chunk held in SGPRs (24 doubles at most: more spill)
+            switch (a.ylist_R * 100 + a.ylist_C) {
+            case 116: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 208: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
+            case 216: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 408: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
+            default: return hipErrorInvalidValue; // df_set_tuning admits the pairs above only
             }
             return hipGetLastError();
         }

@@ -74,6 +74,8 @@ struct RngGeom {
     const PcgJumpDev *jump_block;  // [nblocks]: jump over 4*4096*b outputs
     const PcgJumpDev *jump_thread; // [kRngThreads]: jump over 4*(1024*(tid/64) + tid%64) outputs
     int Nz_g, Pz, z0, z1, is_first, is_last;
+    int yz0, yz1;                  // r_ys columns stored here: [yz0, yz1) at ry column col - yz0 (pitch Pz); [z0, z1),
+                                   // or the strip plus its ghost columns on z-strips that y-filter their own halo
     uint32_t width[6], rows[6];    // row length / row count of each of the six noise arrays
     int debug_flags;               // timing ablations only (wrong results): 1 no log/sqrt, 2 no stores, 4 no redraw,
                                    // 8 no batches (compacted K3: the append loop alone)
@@ -125,6 +127,9 @@ struct SweepArgs {
     // the same as full symmetric vectors (b[|i|], i = -N..N) at tabf + tabf_off[N], 64-B aligned
     const double *tabf;
     const int *tabf_off;
+    // y-pass output: column col of the y-pass plane goes to rz column yout[c] + col when ylo[c] <= col < yhi[c]
+    // (Nzp, 0, Nz_loc; ghost columns: the strip widened by its neighbours' halo columns, Nzp - Gl, ...)
+    int yout[3], ylo[3], yhi[3];
     // z-pass epilogue
     double *filt_old[3], *fluc[3], *filt[3], *T, *rho;
     const double *rowc;     // 7 x Ny: sqrt(R11), b, sqrt(R22-b^2), sqrt(R33), SRA t1, Ts, rhos
@@ -145,7 +150,7 @@ struct SweepArgs {
     // ylds 3 (ypass_t64_kernel): blocks of 4 ylist_R rows x 64 columns, launched in the order ylist[0, ylist_n)
     // (tile = (c * ylist_ncol + column tile) * ylist_nrb + row block; heaviest union of noise rows first)
     const int *ylist;
-    int ylist_n, ylist_nrb, ylist_ncol, ylist_R;
+    int ylist_n, ylist_nrb, ylist_ncol, ylist_R, ylist_C; // R rows per wave, C noise rows per LDS chunk
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

@@ -71,7 +71,7 @@ def test_rccl_strips_match_unsplit_plane(world, mode, replicate):
     check_world(outs, world, replicate)
 
 
-def check_world(outs, world, replicate, Nz=1024):
+def check_world(outs, world, replicate, Nz=1024, ghost=False):
     cols = sorted(o["columns"] for o in outs)
     assert cols[0][0] == 0 and cols[-1][1] == Nz
     assert all(a[1] == b[0] for a, b in zip(cols, cols[1:]))
@@ -81,7 +81,7 @@ def check_world(outs, world, replicate, Nz=1024):
         c = o["comm"]
         assert c["rccl_ranks"] == world
         assert c["rng_collective"] in ((0,) if replicate else (1, 2))  # 2: records in the halo group
-        assert c["halo_peers"] == (0 if world == 1 else (1 if o["rank"] in (0, world - 1) else 2))
+        assert c["halo_peers"] == (0 if world == 1 or ghost else (1 if o["rank"] in (0, world - 1) else 2))
 
 
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
@@ -146,3 +146,28 @@ def test_rccl_run_generation_emulated(world, fused):
         chunk = o["comm"]["rng_blocks_counted"]
         rec = ((chunk * 68 + 7) // 8 * 8 + 8 + 15) // 16 * 16
         assert o["comm"]["rng_bytes_received"] == rec * (world - 1)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("fused", [1, 0])
+def test_rccl_halo_ghost_emulated(world, fused):
+    """Ghost columns (halo_ghost 1, round 5): no halo send/recv at all - each rank y-filters its neighbours'
+    halo columns itself - and the share records all-gathered on the RNG stream (fused 1: right after the
+    counts; 0: the plain per-generation all-gather); every strip bit-equal to the unsplit plane."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(world, "table", 0, Nz=1024, N_min=4, N_max=64, emulate=True,
+                     extra=dict(tuning=dict(gen_dense=2, fused_exchange=fused, halo_ghost=1)))
+    check_world(outs, world, 0, ghost=True)
+    for o in outs:
+        assert o["comm"]["halo_bytes_sent"] == 0 and o["comm"]["halo_peers"] == 0, o["comm"]
+        assert o["comm"]["rng_collective"] == 1, o["comm"]
+
+
+def test_rccl_c4_real_partition_ghost_emulated():
+    """c4 (2048 x 8192, N 4-64) in eight strips with ghost columns: every strip bit-equal to the whole plane."""
+    if n_gpus() < 1:
+        pytest.skip("needs a GPU")
+    outs = run_world(8, "table", 0, Ny=2048, Nz=8192, N_min=4, N_max=64, dts=(1e-8, 1e-5), emulate=True,
+                     extra=dict(tuning=dict(gen_dense=2, halo_ghost=1)))
+    check_world(outs, 8, 0, Nz=8192, ghost=True)

@@ -493,7 +493,15 @@ int gen_set(const df_handle *h, long long g) { return (int)(g % h->nsets); }
 // call (df.cpp:453); the draws depend only on the stream state, so generation n+1
 // is enqueued on rng_stream as soon as call n's sweeps are enqueued, into the
 // other noise set, and runs (compute-bound) under call n's memory-bound sweeps.
-int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
+bool run_form_ok(const df_handle *h)
+{
+    const bool fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024;
+    return h->gen_dense == 2 && h->dense_ready && !fused_plan && h->geom.gen_split == 1;
+}
+
+// allow_run: the run generation may be used (an in-process group takes it only when every strip can, since the
+// strips exchange its share records)
+int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
 {
     const long long gi = h->gen_launched, e = gen_epoch(h, gi);
     const int set = gen_set(h, gi);
@@ -506,7 +514,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs)
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
     g.nb_plan = h->rng_blocks;
     g.fused_plan = h->fuse_plan && !h->split_count && h->rng_blocks <= 1024 ? 1 : 0;
-    g.gen_dense = h->gen_dense == 2 && h->dense_ready && !g.fused_plan && g.gen_split == 1 ? 2 : 0;
+    g.gen_dense = allow_run && run_form_ok(h) ? 2 : 0;
     if (g.gen_dense == 2) { // K1 writes the group counts of its share's record, K2s the share's prefix
         g.xbuf = h->xbuf;
         g.xworld = h->split_count ? h->world : 1;
@@ -562,9 +570,11 @@ int launch_gen_group(std::vector<df_handle *> &hs)
     std::vector<RngGeom> gs(n);
     std::vector<hipStream_t> rss(n);
     int rc;
+    bool run = true; // one form for the whole group: strips set one by one may disagree for a while
+    for (int r = 0; r < n; ++r) run = run && run_form_ok(hs[r]);
     for (int r = 0; r < n; ++r) {
         HIP_OR(hipSetDevice(hs[r]->device), DF_EHIP);
-        if ((rc = gen_begin(hs[r], gs[r], rss[r]))) return rc;
+        if ((rc = gen_begin(hs[r], gs[r], rss[r], run))) return rc;
         HIP_OR(hipEventRecord(hs[r]->ev_counted, rss[r]), DF_EHIP);
     }
     for (int r = 0; r < n; ++r) {

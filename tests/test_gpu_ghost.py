@@ -18,7 +18,7 @@ GHOST = dict(halo_ghost=1)
 
 def check(hs, o, what):
     assert all(h.rng_state() == o.rng.state for h in hs), what
-    for k in FIELDS + ("filt_old_u", "filt_old_v", "filt_old_w"):
+    for k in FIELDS:
         got = np.concatenate([h.field(k) for h in hs], axis=1)
         ref = o.field(k)
         if not np.array_equal(got, ref):

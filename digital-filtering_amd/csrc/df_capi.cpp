@@ -197,7 +197,7 @@ struct df_handle {
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
-    int yt_rows = 2, yt_chunk = 8; // ypass_t64: rows per wave, noise rows per LDS chunk
+    int yt_rows = 2, yt_chunk = 8, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
@@ -373,6 +373,7 @@ SweepArgs sweep_args(df_handle *h)
     a.ylist_ncol = h->ylist_ncol;
     a.ylist_R = h->yt_rows;
     a.ylist_C = h->yt_chunk;
+    a.ylist_PD = h->yt_pd;
     for (int c = 0; c < 3; ++c) {
         a.yout[c] = h->c[c].Nzp;
         a.ylo[c] = 0;
@@ -1326,13 +1327,18 @@ int upload_tables(df_handle *h)
     // no |i| address arithmetic (row-uniform N: every non-grid plane).
     std::vector<int> tabf_off_h(Nmax_all + 1, 0);
     std::vector<double> tabf_h;
+    // kTabGuard zeros before every vector and after the last: ypass_t64 reads a whole chunk's window of taps even
+    // where it hangs past a row's first or last tap, and a zero tap leaves the sum bit for bit (+0 + (+-0) = +0
+    // before the first tap, x + (+-0) = x after the last); the first kTabGuard entries are zeros for rows with
+    // no tap in a chunk. Also the slack of the other sweeps' whole-window scalar loads.
+    constexpr int kTabGuard = 16;
     for (auto &kv : s.coeffs) {
-        tabf_h.resize((tabf_h.size() + 7) / 8 * 8, 0.0);
+        tabf_h.resize((tabf_h.size() + kTabGuard + 7) / 8 * 8, 0.0);
         tabf_off_h[kv.first] = (int)tabf_h.size();
         const int n = kv.first;
         for (int i = -n; i <= n; ++i) tabf_h.push_back(kv.second[i < 0 ? -i : i]);
     }
-    tabf_h.resize(tabf_h.size() + 16, 0.0); // slack for the sweeps' whole-window scalar loads
+    tabf_h.resize(tabf_h.size() + 2 * kTabGuard, 0.0);
     int rc;
     if ((rc = dalloc_t(h, &h->tab, tab_h.size()))) return rc;
     if ((rc = dalloc_t(h, &h->tab_off, tab_off_h.size()))) return rc;
@@ -2364,7 +2370,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"zsplit", h->zsplit},
+        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2397,6 +2403,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
+    } else if (k == "yt_pd") {
+        if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
+        h->yt_pd = value;
     } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 2 x 8, 2 x 16, 4 x 8
         const int R = k == "yt_rows" ? value : h->yt_rows, C = k == "yt_chunk" ? value : h->yt_chunk;
         const int Cd = R == 1 ? 16 : 8; // a row count alone takes its default chunk

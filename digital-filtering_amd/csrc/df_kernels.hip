@@ -1644,6 +1644,14 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
 // vector-memory reads per call hold the y-pass 0.05 ms above its FP64 floor (ablation, profiles/r3/an).
 // Each row adds its taps in the order i = -N..N (noise rows ascending), so results are bit-identical.
 template <int K> using ic_t = std::integral_constant<int, K>;
+// f(ic_t<K>), f(ic_t<K + 1>), ..., f(ic_t<E - 1>): a loop over register sets unrolled at compile time
+template <int K, int E, class F> __device__ __forceinline__ void unroll_to(F &&f)
+{
+    if constexpr (K < E) {
+        f(ic_t<K>{});
+        unroll_to<K + 1, E>(f);
+    }
+}
 
 // PD: chunks of noise loads in flight (register sets; the loop is unrolled by PD so each set stays static)
 // NW waves per block (one block = NW R rows), C noise rows per chunk (C / NW loaded per wave)
@@ -1785,9 +1793,11 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 // noise rows first, components and tiles interleaved, so the widest stencils (N_y 206-212 around j = 160-200)
 // start first instead of wherever their rows fall.
 // Waits: scalar loads return out of order, so while one is in flight every LDS wait is a full lgkmcnt(0). A
-// chunk's R x C coefficients (uniform: one scalar window per row) are therefore loaded before the chunk's
-// barrier, whose wait they share, and the chunk's sums then wait on LDS reads alone. The noise loads of the
-// chunks in flight go to clamped rows instead of being predicated, so their vmcnt waits are counted, not zero.
+// chunk's R x C coefficients (uniform: one scalar window per row, zero taps where the window hangs past the
+// row's range) are therefore loaded before the chunk's barrier, whose wait they share, and the chunk's sums
+// then wait on LDS reads alone; no chunk takes a per-tap path (a scalar load and its wait per tap made a
+// row's first and last chunk cost more than the rest of it). The noise loads of the chunks in flight go to
+// clamped rows instead of being predicated, so their vmcnt waits are counted, not zero.
 // Each row adds its taps in the order i = -N..N (noise rows ascending) with df.cpp:373-375's products:
 // bit-identical to every other form.
 template <int R, int NW, int C, int PD>
@@ -1842,72 +1852,64 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 #pragma unroll
         for (int k = 0; k < LP; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
     };
-    auto is_full = [&](int u0) { // every row of the wave takes all C noise rows of the chunk
-        bool f = u0 + C - 1 <= mhi;
+    // Every chunk takes the whole-window path: a row's window may hang past its first or last tap into the
+    // table's zero guards (kTabGuard >= C, df_capi.cpp upload_tables), and a row with no tap in the chunk reads
+    // the zeros at the table's start; zero taps leave each sum bit for bit.
+    auto live = [&](int u0) { // some row of the wave has a tap in the chunk
+        bool f = false;
 #pragma unroll
-        for (int r = 0; r < R; ++r) f = f && lo[r] <= u0 && hi[r] >= u0 + C - 1;
+        for (int r = 0; r < R; ++r) f = f || (lo[r] <= u0 + C - 1 && hi[r] >= u0);
         return f;
     };
-    double cw[R][C]; // a full chunk's coefficients (uniform)
+    double cw[R][C]; // the chunk's coefficients (uniform)
     auto cload = [&](int u0) {
 #pragma unroll
-        for (int r = 0; r < R; ++r)
+        for (int r = 0; r < R; ++r) {
+            const double *src = lo[r] <= u0 + C - 1 && hi[r] >= u0 ? tb[r] + (u0 - lo[r]) : a.tabf;
 #pragma unroll
-            for (int q = 0; q < C; ++q) cw[r][q] = tb[r][u0 - lo[r] + q];
+            for (int q = 0; q < C; ++q) cw[r][q] = src[q];
+        }
     };
     double acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = 0.0;
-    auto compute = [&](int u0, int buf, bool full) {
-        if (full) {
+    auto compute = [&](int buf, bool on) {
+        if (!on) return;
 #pragma unroll
-            for (int p = 0; p < C / 2; ++p) {
-                const dvec2 n = nbuf[buf][p][lane];
+        for (int p = 0; p < C / 2; ++p) {
+            const dvec2 n = nbuf[buf][p][lane];
 #pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p] * n.x;
+            for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p] * n.x;
 #pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p + 1] * n.y;
-            }
-            return;
-        }
-        const int mb = min(u0 + C - 1, mhi);
-        bool any = false;
-#pragma unroll
-        for (int r = 0; r < R; ++r) any = any || (lo[r] <= mb && hi[r] >= u0);
-        if (!any) return;
-        for (int m = u0; m <= mb; ++m) {
-            const dvec2 n2 = nbuf[buf][(m - u0) >> 1][lane];
-            const double n = ((m - u0) & 1) ? n2.y : n2.x;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (m >= lo[r] && m <= hi[r]) acc[r] += tb[r][m - lo[r]] * n; // wave-uniform
+            for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p + 1] * n.y;
         }
     };
     // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
     // ypass_tlds_kernel); its coefficients (full chunks) loaded before the barrier that precedes it
     const int nch = (mhi - mlo) / C + 1;
-    gload(ic_t<0>{}, mlo);
-    if constexpr (PD > 1) gload(ic_t<1 % PD>{}, mlo + C);
+    // prologue: chunks 0 .. PD - 1 in flight, chunk 0 staged
+    unroll_to<0, PD>([&](auto K) { gload(K, mlo + decltype(K)::value * C); });
     lstore(ic_t<0>{}, 0);
-    bool full = is_full(mlo);
-    if (full) cload(mlo);
+    bool on = live(mlo);
+    if (on) cload(mlo);
     __syncthreads();
     auto step = [&](auto K, int i) {
         constexpr int k = decltype(K)::value;
-        if (i + PD < nch) gload(K, mlo + (i + PD) * C); // block-uniform
-        compute(mlo + i * C, i & 1, full);
+        // chunk i + PD into the set chunk i left - unconditionally (rows clamped to mhi past the end), so the
+        // count of loads in flight is fixed and the waits below are counted vmcnt(n), not vmcnt(0)
+        gload(K, mlo + (i + PD) * C);
+        compute(i & 1, on);
         if (i + 1 < nch) {
             lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
-            full = is_full(mlo + (i + 1) * C);
-            if (full) cload(mlo + (i + 1) * C);
+            on = live(mlo + (i + 1) * C);
+            if (on) cload(mlo + (i + 1) * C);
         }
         __syncthreads();
     };
-    for (int i = 0; i < nch; i += PD) {
-        step(ic_t<0>{}, i);
-        if constexpr (PD > 1)
-            if (i + 1 < nch) step(ic_t<1 % PD>{}, i + 1);
-    }
+    for (int i = 0; i < nch; i += PD)
+        unroll_to<0, PD>([&](auto K) {
+            if (i + decltype(K)::value < nch) step(K, i + decltype(K)::value);
+        });
     if (col < a.ylo[c] || col >= a.yhi[c]) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1924,11 +1926,15 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
         if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
             const dim3 grid((unsigned)a.ylist_n);
             // R x C coefficients of a chunk held in SGPRs (24 doubles at most: more spill)
-            switch (a.ylist_R * 100 + a.ylist_C) {
-            case 116: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-            case 208: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
-            case 216: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-            case 408: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
+            switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
+            case 1162: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 1164: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 4>), grid, dim3(256), 0, st, a); break;
+            case 2082: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
+            case 2084: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 4>), grid, dim3(256), 0, st, a); break;
+            case 2162: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+            case 2164: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 4>), grid, dim3(256), 0, st, a); break;
+            case 4082: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
+            case 4084: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 4>), grid, dim3(256), 0, st, a); break;
             default: return hipErrorInvalidValue; // df_set_tuning admits the pairs above only
             }
             return hipGetLastError();

@@ -150,7 +150,8 @@ struct SweepArgs {
     // ylds 3 (ypass_t64_kernel): blocks of 4 ylist_R rows x 64 columns, launched in the order ylist[0, ylist_n)
     // (tile = (c * ylist_ncol + column tile) * ylist_nrb + row block; heaviest union of noise rows first)
     const int *ylist;
-    int ylist_n, ylist_nrb, ylist_ncol, ylist_R, ylist_C; // R rows per wave, C noise rows per LDS chunk
+    int ylist_n, ylist_nrb, ylist_ncol, ylist_R, ylist_C, ylist_PD; // R rows per wave, C noise rows per LDS chunk,
+                                                                     // PD chunks of noise loads in flight
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

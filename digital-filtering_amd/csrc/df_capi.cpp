@@ -197,7 +197,7 @@ struct df_handle {
     long long gen_base = 0; // generation that starts epoch 0 (reset whenever the prefetched noise is discarded)
     int cur = 0;                // noise set of the current step
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
-    int yt_rows = 2, yt_chunk = 8, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
+    int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
@@ -1130,10 +1130,11 @@ int plan_strips(df_handle *h)
             h->rows_per_wave = 1;
             h->yunroll = 8;
         } else h->rows_per_wave = 2;
-        // table mode, long chains: the noise staged in LDS per block of 4 rows, 2 chunks in flight (ylds): the
-        // reference's grid y-pass 0.051 -> 0.043 ms, call -9%; c3 and c2 (short chains, FP64-issue-bound) lose
-        // with it (profiles/r3/bd)
-        if (h->coeff_mode == DF_COEFF_TABLE && long_chain) h->ylds = 2;
+        // table mode, long chains: the noise staged in LDS per block of rows (ylds): round 3's ypass_tlds (the
+        // reference's grid y-pass 0.051 -> 0.043 ms, call -9%, profiles/r3/bd), round 5's ypass_t64 (64-column
+        // tiles, one cell and one row per lane, heaviest blocks first, whole-window chunks: 40.4 -> 24.7 us alone,
+        // profiles/r5). c3 and c2 (short chains, FP64-issue-bound) lose with LDS staging.
+        if (h->coeff_mode == DF_COEFF_TABLE && long_chain) h->ylds = s.per_cell ? 2 : 3;
         // Long chains, packed: one block per row pair, noise loads shared by both rows, the next chunk in
         // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
         // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
@@ -2405,17 +2406,18 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {
         if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
+        if (value == 4 && h->yt_rows != 1) return fail(DF_EINVAL, "yt_pd 4 is built for yt_rows 1 only");
         h->yt_pd = value;
-    } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 2 x 8, 2 x 16, 4 x 8
+    } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 2 x 8, 2 x 16
         const int R = k == "yt_rows" ? value : h->yt_rows, C = k == "yt_chunk" ? value : h->yt_chunk;
-        const int Cd = R == 1 ? 16 : 8; // a row count alone takes its default chunk
-        const int Cu = k == "yt_rows" && !(R == 2 && (C == 8 || C == 16)) ? Cd : C;
-        if (!((R == 1 && Cu == 16) || (R == 2 && (Cu == 8 || Cu == 16)) || (R == 4 && Cu == 8)))
-            return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 2 x 8, 2 x 16 or 4 x 8");
+        const int Cu = k == "yt_rows" && !(R == 2 && C == 8) ? 16 : C; // a row count alone takes chunks of 16
+        if (!((R == 1 && Cu == 16) || (R == 2 && (Cu == 8 || Cu == 16))))
+            return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 2 x 8 or 2 x 16");
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
         h->yt_rows = R;
         h->yt_chunk = Cu;
+        if (R != 1) h->yt_pd = 2;
         if (int rc = build_ylists(h)) return rc;
     }
     else if (k == "halo_ghost") { // the same on every rank of a plane (it decides whether a halo exchange runs)

@@ -1862,12 +1862,12 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         return f;
     };
     double cw[R][C]; // the chunk's coefficients (uniform)
-    auto cload = [&](int u0) {
+    auto cload = [&](double (&dst)[R][C], int u0) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const double *src = lo[r] <= u0 + C - 1 && hi[r] >= u0 ? tb[r] + (u0 - lo[r]) : a.tabf;
 #pragma unroll
-            for (int q = 0; q < C; ++q) cw[r][q] = src[q];
+            for (int q = 0; q < C; ++q) dst[r][q] = src[q];
         }
     };
     double acc[R];
@@ -1891,7 +1891,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     unroll_to<0, PD>([&](auto K) { gload(K, mlo + decltype(K)::value * C); });
     lstore(ic_t<0>{}, 0);
     bool on = live(mlo);
-    if (on) cload(mlo);
+    if (on) cload(cw, mlo);
     __syncthreads();
     auto step = [&](auto K, int i) {
         constexpr int k = decltype(K)::value;
@@ -1902,7 +1902,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         if (i + 1 < nch) {
             lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
             on = live(mlo + (i + 1) * C);
-            if (on) cload(mlo + (i + 1) * C);
+            if (on) cload(cw, mlo + (i + 1) * C);
         }
         __syncthreads();
     };
@@ -1926,15 +1926,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
         if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
             const dim3 grid((unsigned)a.ylist_n);
             // R x C coefficients of a chunk held in SGPRs (24 doubles at most: more spill)
+            // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 2 x 16 26.6, 2 x 8 35-39, the
+            // round-4 ypass_tlds 40.4; 4 chunks in flight lose (VGPRs 38 -> 114) except on a lone block
             switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
             case 1162: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
             case 1164: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 4>), grid, dim3(256), 0, st, a); break;
             case 2082: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
-            case 2084: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 4>), grid, dim3(256), 0, st, a); break;
             case 2162: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-            case 2164: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 4>), grid, dim3(256), 0, st, a); break;
-            case 4082: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
-            case 4084: hipLaunchKernelGGL((ypass_t64_kernel<4, 4, 8, 4>), grid, dim3(256), 0, st, a); break;
             default: return hipErrorInvalidValue; // df_set_tuning admits the pairs above only
             }
             return hipGetLastError();

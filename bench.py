@@ -858,6 +858,38 @@ def main(argv=None):
         if oname == "c5" and ctx.world > 1 and args.long_run == "auto":
             others[oname]["long_run"] = long_run(dfamd, ctx, owl, args, 10000, ctx.comm_id(dfamd))
 
+    if ctx.world == 1 and "native" in others and args.alt_modes == "auto" and args.coeff_mode == "packed":
+        # the reference's own grid in table mode - the C/C++/Fortran drop-in default on the only plane the
+        # reference computes - with its FP64 roofline, as alt_modes.table for c3
+        owl = plan_workload("native", ctx.world, args.scaling)
+        g = make_filter(dfamd, ctx, owl, args, "table")
+        taps = sum(g.comp_info(c)["by_size"] + g.comp_info(c)["bz_size"] for c in range(3))
+        el2, _, n2 = timed(ctx, g, args, min_warm_s=0.3, profile=False, label="native table")
+        el2p, p2, n3 = timed(ctx, g, args, label="native table, phase events")
+        ms2 = el2 * 1e3 / args.steps
+        cells = owl["Ny"] * owl["Nz"]
+        sw_ms = (p2["ypass_ms"] + p2["zpass_ms"]) / max(1, p2["calls"])
+        tf = 2.0 * taps / (sw_ms * 1e-3) / 1e12
+        nt = {"workload": owl["desc"] + ", table mode", "Ny": owl["Ny"], "Nz": owl["Nz"],
+              "value": round(cells * args.steps / el2, 1), "ms_per_step": round(ms2, 4),
+              "ms_per_step_with_phase_events": round(el2p * 1e3 / args.steps, 4), "phase_ms_per_call": per_call(p2),
+              "launch_shape": {k: g.get_tuning(k) for k in ("ylds", "yt_rows", "yt_chunk", "handoff_batch", "gen_dense")},
+              "roofline_valu": {"bound": "valu-fp64", "achieved": round(tf, 2), "peak": 78.6, "unit": "TFLOP/s",
+                                "frac": round(tf / 78.6, 4), "flops_per_call": 2.0 * taps, "sweeps_ms": round(sw_ms, 4),
+                                "note": "2 flop per tap and cell over the y- and z-pass phase time (hipEvents; the "
+                                        "RNG of later calls runs beside them); mul+add without FMA caps at 39.3"}}
+        vp = os.path.join(ROOT, "profiles", "r1", "probe", "valu_probe_fp64.jsonl")
+        if os.path.exists(vp):
+            best = max(json.loads(l)["wave_instr_per_s"] for l in open(vp) if l.startswith("{"))
+            nt["roofline_valu"]["measured_ceiling"] = {"TFLOPs": round(best * 64 / 1e12, 1),
+                                                       "frac": round(tf / (best * 64 / 1e12), 4),
+                                                       "source": os.path.relpath(vp, ROOT)}
+        if args.parity == "on":
+            ops = ctx.gather(parity_check(dfamd, ctx, owl, args, g, n2 + n3))
+            nt["parity_ok"] = all(p["ok"] for p in ops)
+        g.close()
+        others["native_table"] = nt
+
     dropin = None
     rank_phase("reports (drop-in, CPU baseline, JSON line)")
     if ctx.rank == 0 and ctx.world == 1 and args.dropin == "auto":

@@ -214,8 +214,10 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   8-deep load ring of long chains), "ycoop" (packed y-pass: 7 = a block per row pair, the long-chain
  *   default; 0 = a wave per tile), "ycoop_order" (row-pair dispatch inside each XCD run: 0 ascending,
  *   g >= 1 groups of g tiles heaviest first; 4 on long chains), "ylds" (table y-pass with LDS-staged noise:
- *   2 = a block per (strip, 4 rows), 3 = a block per (64 columns, 4 "yt_rows" rows), heaviest first;
- *   0 = a wave per tile), "yt_rows" (1, 2, 4, 8: rows per wave of ylds 3), "zsplit" (packed z-pass, a wave
+ *   2 = a block per (strip, 4 rows), 3 = a block per (64 columns, 4 waves of "yt_rows" rows) walking the
+ *   tap window in "yt_chunk"-row chunks through a double-buffered LDS ring, "yt_pd" chunks of noise loads
+ *   in flight, heaviest first; 0 = a wave per tile), "yt_rows" x "yt_chunk" (1 x 16 default, 2 x 8,
+ *   2 x 16), "yt_pd" (2; 4 for yt_rows 1: deeper prefetch, more VGPRs), "zsplit" (packed z-pass, a wave
  *   per component: few-tile planes), "zstage" (table z-pass noise staged in LDS: 2 default, 0 the unstaged
  *   form large halos take), "nt_stores" (non-temporal output stores), "ywin_T" / "ywin_W" / "zwin_T" /
  *   "zwin_W" (sweep write windows: packed planes streaming >= 2 GB of coefficients).
@@ -231,7 +233,9 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   grouped RCCL operation per call; 0 = an all-gather of their own), "halo_overlap" (1 = send/recv, unpack
  *   and edge-strip z-pass on a high-priority stream under the interior strips' z-pass; 0 = one serial
  *   chain; -1 default = 1 packed, 0 table), "halo_loopback" (one-rank RCCL handle: send the halo to itself
- *   and check it). */
+ *   and check it), "halo_ghost" (table mode, row-uniform planes, same on every rank: 1 = each strip
+ *   y-filters its neighbours' halo columns itself from the same noise, no halo exchange; the share records'
+ *   all-gather runs on the noise stream ahead of the call). */
 int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* The launch shape the handle will use for a df_set_tuning key: the plane-dependent defaults chosen at

@@ -107,7 +107,7 @@ struct df_handle {
     ncclComm_t comm = nullptr;
     int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
     int rows_per_wave = 8;
-    int yunroll = 2, zunroll = 4; // z: 8 taps in flight per iteration (measured -1..3%); y: 4x body neutral
+    int yunroll = 2, zunroll = 4; // z: 8 taps per step (-1..3% against 4; 16 taps +0..6%, profiles/r5/zu)
     int nt_stores = 1; // outputs streamed past the caches (same-handle A/B: -1.5% per call)
     int ynt_stores = 1; // the y-pass output likewise
     int ywin_T = 0, ywin_W = 0, zwin_T = 0, zwin_W = 0; // sweep write windows (SweepArgs)

@@ -2120,53 +2120,31 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         double acc0 = 0.0, acc1 = 0.0;
         double2 P = ld_pair(xp);
         int m = 0;
-        if (ZU >= 4) {
-            for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
-                const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2), P3 = ld_pair(xp + m + 3), P4 = ld_pair(xp + m + 4);
-                double2 b[8];
+        // K noise pairs (2K taps) per step: the 2K coefficient loads and K pair loads issued first, then the
+        // products added in tap order (acc0: taps 2u with P[u].x, 2u+1 with P[u].y; acc1 one column on)
+        auto step = [&](auto KC) {
+            constexpr int K = decltype(KC)::value;
+            for (; m + K <= N; m += K) {
+                double2 Pn[K + 1];
+                Pn[0] = P;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) b[u] = coef(2 * m + u);
-                acc0 += b[0].x * P.x;
-                acc1 += b[0].y * P.y;
-                acc0 += b[1].x * P.y;
-                acc1 += b[1].y * P1.x;
-                acc0 += b[2].x * P1.x;
-                acc1 += b[2].y * P1.y;
-                acc0 += b[3].x * P1.y;
-                acc1 += b[3].y * P2.x;
-                acc0 += b[4].x * P2.x;
-                acc1 += b[4].y * P2.y;
-                acc0 += b[5].x * P2.y;
-                acc1 += b[5].y * P3.x;
-                acc0 += b[6].x * P3.x;
-                acc1 += b[6].y * P3.y;
-                acc0 += b[7].x * P3.y;
-                acc1 += b[7].y * P4.x;
-                P = P4;
+                for (int u = 1; u <= K; ++u) Pn[u] = ld_pair(xp + m + u);
+                double2 b[2 * K];
+#pragma unroll
+                for (int u = 0; u < 2 * K; ++u) b[u] = coef(2 * m + u);
+#pragma unroll
+                for (int u = 0; u < K; ++u) {
+                    acc0 += b[2 * u].x * Pn[u].x;
+                    acc1 += b[2 * u].y * Pn[u].y;
+                    acc0 += b[2 * u + 1].x * Pn[u].y;
+                    acc1 += b[2 * u + 1].y * Pn[u + 1].x;
+                }
+                P = Pn[K];
             }
-        }
-        for (; m + 2 <= N; m += 2) {
-            const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2);
-            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
-            acc0 += b0.x * P.x;
-            acc1 += b0.y * P.y;
-            acc0 += b1.x * P.y;
-            acc1 += b1.y * P1.x;
-            acc0 += b2.x * P1.x;
-            acc1 += b2.y * P1.y;
-            acc0 += b3.x * P1.y;
-            acc1 += b3.y * P2.x;
-            P = P2;
-        }
-        for (; m < N; ++m) {
-            const double2 P1 = ld_pair(xp + m + 1);
-            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1);
-            acc0 += b0.x * P.x;
-            acc1 += b0.y * P.y;
-            acc0 += b1.x * P.y;
-            acc1 += b1.y * P1.x;
-            P = P1;
-        }
+        };
+        if constexpr (ZU >= 4) step(ic_t<4>{});
+        step(ic_t<2>{});
+        step(ic_t<1>{});
         const double2 bl = coef(2 * N);
         acc0 += bl.x * P.x;
         acc1 += bl.y * P.y;
@@ -2273,20 +2251,16 @@ hipError_t launch_zpass(const SweepArgs &a, bool table, hipStream_t st)
     const long long tiles = (long long)a.zs_n * a.Ny;
     if (tiles <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((tiles + 3) / 4);
-    const bool u4 = a.zunroll >= 4;
     if (table && a.per_cell) {
         hipLaunchKernelGGL((zpass_kernel<true, false, 4, true>), dim3(blocks), dim3(256), 0, st, a);
     } else if (table) {
         const size_t lds = a.zstage && a.zgroup ? 3 * (size_t)a.zstage_reg * sizeof(double) : 0;
         const dim3 grid(a.zgroup ? (unsigned)(a.Ny * ((a.zs_n + 3) / 4)) : blocks);
-        if (u4) hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), grid, dim3(256), lds, st, a);
-        else hipLaunchKernelGGL((zpass_kernel<true, false, 2, false>), grid, dim3(256), lds, st, a);
+        hipLaunchKernelGGL((zpass_kernel<true, false, 4, false>), grid, dim3(256), lds, st, a);
     } else if (a.zsplit) { // packed, one 3-wave block per tile
         hipLaunchKernelGGL((zpass_kernel<false, true, 4, false, true>), dim3((unsigned)tiles), dim3(192), 0, st, a);
-    } else if (u4) {
-        hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
     } else {
-        hipLaunchKernelGGL((zpass_kernel<false, true, 2, false>), dim3(blocks), dim3(256), 0, st, a);
+        hipLaunchKernelGGL((zpass_kernel<false, true, 4, false>), dim3(blocks), dim3(256), 0, st, a);
     }
     return hipGetLastError();
 }

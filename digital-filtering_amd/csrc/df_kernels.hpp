@@ -136,7 +136,7 @@ struct SweepArgs {
     double sa[3], s1a[3];   // sqrt(alpha), sqrt(1-alpha) per component
     int do_corr, do_sra, comps_mask;
     int write_filt;         // stage API: z-pass stores filt[c] only (df.cpp:401)
-    int yunroll, zunroll;   // taps per loop iteration: packed y 2, 4, 8 (deep ring); z 2, 4
+    int yunroll, zunroll;   // taps per loop iteration: packed y 2, 4, 8 (deep ring); z pairs per step 4
     int nt_stores;          // z-pass outputs stored non-temporally
     int ynt_stores;         // y-pass output (r_zs) stored non-temporally
     int zstage;             // table z-pass: a block's 4 strips of one row read their noise from LDS (2: 16-B copy,

@@ -45,6 +45,9 @@ def parse(outdir, counter):
 
 
 def short(name):
+    for k in ("ypass", "zpass"):  # every y-pass form (packed, coop2, table, t64, tlds) is the launch's y-pass
+        if k + "_" in name:
+            return k + "_kernel"
     for k in ("ypass_kernel", "zpass_kernel", "rng_generate_kernel", "rng_count_kernel", "expand_coeffs_kernel",
               "read_kernel<false>", "read_kernel<true>", "write_kernel<1>", "write_kernel<2>"):
         if k in name:
@@ -62,25 +65,27 @@ def collapse(per):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc"))
-    ap.add_argument("--config", default="c3")
-    ap.add_argument("--modes", default="packed,table")
+    ap.add_argument("--configs", default="c3:packed+table,c2:packed,native:packed,c1:packed",
+                    help="config:mode+mode,... (the N = 1 bench line's planes)")
     ap.add_argument("--json", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"))  # copy to profiles/
     a = ap.parse_args()
     a.out, a.json = os.path.abspath(a.out), os.path.abspath(a.json)  # rocprofv3 runs from /tmp
     probe = [os.path.join(ROOT, "tools", "hbm_probe"), "pmc"]
-    res = {"method": __doc__.strip().splitlines()[0], "config": a.config, "raw_kib": {}, "per_launch_bytes": {}}
+    plan = [(c.split(":")[0], m) for c in a.configs.split(",") for m in c.split(":")[1].split("+")]
+    res = {"method": __doc__.strip().splitlines()[0], "configs": a.configs, "raw_kib": {}, "per_launch_bytes": {}}
     raw = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(a.out, f"probe_{counter}")
         run_pmc(counter, d, probe)
         raw[("probe", counter)] = collapse(parse(d, counter))
-        for mode in a.modes.split(","):
-            d = os.path.join(a.out, f"{mode}_{counter}")
-            run_pmc(counter, d, [sys.executable, os.path.join(ROOT, "bench.py"), "--config", a.config,
+        for cfg, mode in plan:
+            d = os.path.join(a.out, f"{cfg}_{mode}_{counter}")
+            run_pmc(counter, d, [sys.executable, os.path.join(ROOT, "bench.py"), "--config", cfg,
                                  "--coeff-mode", mode, "--steps", "3", "--warmup", "1", "--cpu-baseline", "off",
                                  "--alt-modes", "off", "--other-configs", "", "--parity", "off"])
-            raw[(mode, counter)] = collapse(parse(d, counter))
+            raw[(cfg, mode, counter)] = collapse(parse(d, counter))
     gib = float(1 << 30)
+    raw = {(k[0], k[1]) if k[0] == "probe" else k: v for k, v in raw.items()}
     pf = raw[("probe", "FETCH_SIZE")]
     pw = raw[("probe", "WRITE_SIZE")]
     cal = {
@@ -90,23 +95,23 @@ def main():
         "write16_factor": gib / (statistics.median(pw["write_kernel<2>"]) * 1024),
     }
     res["calibration"] = cal
-    for mode in a.modes.split(","):
-        f = raw[(mode, "FETCH_SIZE")]
-        w = raw[(mode, "WRITE_SIZE")]
+    for cfg, mode in plan:
+        f = raw[(cfg, mode, "FETCH_SIZE")]
+        w = raw[(cfg, mode, "WRITE_SIZE")]
         for k, wfac in (("ypass_kernel", cal["write16_factor"]), ("zpass_kernel", cal["write8_factor"])):
             if k not in f or k not in w:
                 continue
             fk = statistics.median(f[k][1:] if len(f[k]) > 1 else f[k])  # skip the constructor's step 0
             wk = statistics.median(w[k][1:] if len(w[k]) > 1 else w[k])
             rfac = cal["read16_nt_factor"] if mode == "packed" else cal["read16_factor"]
-            key = f"{a.config}/{mode}/{k.split('_')[0]}"
+            key = f"{cfg}/{mode}/{k.split('_')[0]}"
             res["per_launch_bytes"][key] = fk * 1024 * rfac + wk * 1024 * wfac
             res["raw_kib"][key] = {"FETCH_SIZE": fk, "WRITE_SIZE": wk}
         for k in ("rng_generate_kernel", "rng_count_kernel"):
             if k in f and k in w:
-                res["raw_kib"][f"{a.config}/{mode}/{k}"] = {"FETCH_SIZE": statistics.median(f[k]),
+                res["raw_kib"][f"{cfg}/{mode}/{k}"] = {"FETCH_SIZE": statistics.median(f[k]),
                                                            "WRITE_SIZE": statistics.median(w[k])}
-    res["raw_kib"]["probe"] = {f"{c}:{k}": statistics.median(v) for (m, c), d in raw.items() if m == "probe"
+    res["raw_kib"]["probe"] = {f"{key[1]}:{k}": statistics.median(v) for key, d in raw.items() if key[0] == "probe"
                                for k, v in d.items()}
     os.makedirs(os.path.dirname(a.json), exist_ok=True)
     json.dump(res, open(a.json, "w"), indent=1)

@@ -88,7 +88,14 @@ struct CompDev {
 struct PhaseEvents {
     hipEvent_t e[6]; // main stream: start, after ypass, after halo, after zpass; RNG stream: start, end
     bool rng = false;
+    bool ahead = false; // the call's y-pass ran ahead on ystream (timed by YEvents, not e[0] -> e[1])
     int gens = 0; // generations enqueued during the call: e[4] before the first, e[5] after the last
+};
+
+// An epoch's y-passes run ahead on ystream, timed as one span (profiling)
+struct YEvents {
+    hipEvent_t e[2];
+    int n = 0; // y-passes between e[0] and e[1]
 };
 
 } // namespace
@@ -103,6 +110,16 @@ struct df_handle {
     hipStream_t stream = nullptr;     // sweeps (memory-bound)
     hipStream_t rng_stream = nullptr; // noise generation for the NEXT call (compute-bound), overlapped
     hipEvent_t ev_rng[2] = {}, ev_release[2] = {};
+    // Y-pass ahead (round 5): the y-pass reads only its generation's r_ys and writes only that set's r_zs
+    // interior, and depends on nothing a call changes, so it runs on ystream as soon as its epoch's noise is
+    // ready, calls ahead of the call that consumes it; the stream then waits for ev_swept instead of ev_rng and
+    // runs the halo and the z-pass alone. ep_swept: the epoch (by parity) was swept ahead; cur_swept: the
+    // current step's set was.
+    int yahead = 0;
+    hipStream_t ystream = nullptr;
+    hipEvent_t ev_swept[2] = {};
+    bool ep_swept[2] = {false, false};
+    bool cur_swept = false;
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
     int Nz_g = 0, z0 = 0, z1 = 0, Nz_loc = 0, nstrips = 0, Pz = 0, Ny = 0;
@@ -231,6 +248,11 @@ struct df_handle {
     df_profile prof{};
     double prof_rng_span = 0; // RNG stream time of the profiled calls' generation bursts (ms)
     long long prof_rng_gens = 0; // generations in those bursts
+    std::vector<YEvents> yev;   // ahead y-pass spans (every profile_every-th epoch)
+    size_t yev_used = 0;
+    long long yev_seq = 0;
+    double prof_y_span = 0, prof_y_main = 0; // ms: ahead spans; y-passes on the stream
+    long long prof_y_n = 0, prof_y_calls = 0; // y-passes in the spans; profiled calls whose y-pass ran ahead
     std::vector<void *> allocs;
 };
 
@@ -444,6 +466,7 @@ void ev_record(df_handle *h, int phase, hipStream_t st = nullptr)
 int sync_all(df_handle *h)
 {
     HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
+    if (h->ystream) HIP_OR(hipStreamSynchronize(h->ystream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     if (h->comm_stream) HIP_OR(hipStreamSynchronize(h->comm_stream), DF_EHIP);
     return DF_OK;
@@ -463,7 +486,8 @@ int drain_profile(df_handle *h)
             h->prof_rng_span += r;
             h->prof_rng_gens += h->ev[i].gens;
         }
-        h->prof.ypass_ms += t[0];
+        if (h->ev[i].ahead) h->prof_y_calls++;
+        else h->prof_y_main += t[0];
         h->prof.halo_ms += t[1];
         h->prof.zpass_ms += t[2];
         h->prof.total_ms += tot;
@@ -472,6 +496,15 @@ int drain_profile(df_handle *h)
         h->ev[i].gens = 0;
     }
     h->ev_used = 0;
+    for (size_t i = 0; i < h->yev_used; ++i) {
+        float y = 0;
+        (void)hipEventElapsedTime(&y, h->yev[i].e[0], h->yev[i].e[1]);
+        h->prof_y_span += y;
+        h->prof_y_n += h->yev[i].n;
+    }
+    h->yev_used = 0;
+    // an ahead call's y-pass time: the measured time per ahead y-pass (its epoch's span / its y-passes)
+    h->prof.ypass_ms = h->prof_y_main + (h->prof_y_n ? h->prof_y_span / (double)h->prof_y_n * (double)h->prof_y_calls : 0.0);
     // Every call consumes one generation, but with hand-off batches (hb > 1) a call enqueues a burst of hb
     // generations at an epoch start and none mid-epoch, and sampled profiling may always land on the same
     // epoch position: rng_ms is therefore the measured time per generation times the calls profiled.
@@ -544,7 +577,28 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
     return DF_OK;
 }
 
-int phase_ypass(df_handle *h, int comps_mask);
+int phase_ypass(df_handle *h, int comps_mask, int set = -1, hipStream_t st = nullptr);
+
+// The epoch just generated: its y-passes on ystream, ev_swept after them (df_handle::yahead)
+int sweep_ahead(df_handle *h, long long e, hipStream_t rs)
+{
+    const bool on = h->yahead && h->overlap && h->ystream;
+    h->ep_swept[e & 1] = on;
+    if (!on) return DF_OK;
+    HIP_OR(hipStreamWaitEvent(h->ystream, h->ev_rng[e & 1], 0), DF_EHIP);
+    const bool timed = h->profiling && (h->yev_seq++ % h->profile_every) == 0 && h->yev_used < h->yev.size();
+    if (timed) HIP_OR(hipEventRecord(h->yev[h->yev_used].e[0], h->ystream), DF_EHIP);
+    const long long g0 = h->hb == 1 ? e : h->gen_base + e * h->hb;
+    for (long long g = g0; g < g0 + h->hb; ++g)
+        if (int rc = phase_ypass(h, 7, gen_set(h, g), h->ystream)) return rc;
+    if (timed) {
+        HIP_OR(hipEventRecord(h->yev[h->yev_used].e[1], h->ystream), DF_EHIP);
+        h->yev[h->yev_used++].n = h->hb;
+    }
+    HIP_OR(hipEventRecord(h->ev_swept[e & 1], h->ystream), DF_EHIP);
+    (void)rs;
+    return DF_OK;
+}
 
 int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
 {
@@ -557,8 +611,11 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
                              h->rng_blocks, nb_scan, rs),
            DF_EHIP);
     if (prof_on(h)) ev_record(h, 5, rs);
-    if (gen_pos(h, gi) == h->hb - 1) // the epoch's noise is ready
+    if (gen_pos(h, gi) == h->hb - 1) { // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
+        h->gen_launched++;
+        return sweep_ahead(h, gen_epoch(h, gi), rs);
+    }
     h->gen_launched++;
     return DF_OK;
 }
@@ -659,7 +716,8 @@ int consume_gen(df_handle *h)
     const long long need = h->hb == 1 ? gi + 1 : h->gen_base + (e + 1) * h->hb; // this epoch, launched
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
-    if (first) HIP_OR(hipStreamWaitEvent(h->stream, h->ev_rng[e & 1], 0), DF_EHIP);
+    h->cur_swept = h->ep_swept[e & 1];
+    if (first) HIP_OR(hipStreamWaitEvent(h->stream, (h->cur_swept ? h->ev_swept : h->ev_rng)[e & 1], 0), DF_EHIP);
     h->cur = gen_set(h, gi);
     h->gen_used++;
     return DF_OK;
@@ -732,10 +790,15 @@ int fused_gen_end(df_handle *h)
     return gen_end(h, h->pend_g, rs);
 }
 
-int phase_ypass(df_handle *h, int comps_mask)
+int phase_ypass(df_handle *h, int comps_mask, int set, hipStream_t st)
 {
     SweepArgs a = sweep_args(h);
     a.comps_mask = comps_mask;
+    if (set >= 0)
+        for (int c = 0; c < 3; ++c) {
+            a.ry[c] = h->c[c].ry[set];
+            a.rz[c] = h->c[c].rz[set];
+        }
     if (h->ghost) { // the strip widened by its ghost columns; each component keeps the Nzp columns its halo holds
         a.Nz_loc = h->Wext;
         a.nstrips = h->nstrips_g;
@@ -750,7 +813,7 @@ int phase_ypass(df_handle *h, int comps_mask)
             a.yhi[c] = std::min(h->Wext, h->Gl + h->Nz_loc + (h->Gr ? h->c[c].Nzp : 0));
         }
     }
-    HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, h->stream), DF_EHIP);
+    HIP_OR(launch_ypass(a, h->coeff_mode == DF_COEFF_TABLE, h->rows_per_wave, st ? st : h->stream), DF_EHIP);
     return DF_OK;
 }
 
@@ -1146,6 +1209,11 @@ int plan_strips(df_handle *h)
             h->ycoop = 7;
             h->ycoop_order = 4;
         }
+        // Long chains, both modes: the y-pass runs ahead on its own stream (df_handle::yahead), so a call's
+        // z-pass shares the chip with later calls' y-passes instead of idling beside its own latency-bound tail
+        // (same handle A/B, 9 rounds: the reference's grid packed 0.194 -> 0.165 ms, table 0.060 -> 0.055;
+        // c1 even; HBM-bound c2 +9%, c3 +0.6..1%: two streaming passes at once only contend; profiles/r5/d)
+        if (long_chain) h->yahead = 1;
         // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
         // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
         // profiles/r2/ab_zsplit.jsonl)
@@ -1290,6 +1358,7 @@ int open_device(df_handle *h, int device)
     const int use_prio = 0; // measured: priorities cost 1-2% wall time (in-process A/B, tools/ab.py)
     HIP_OR(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, use_prio ? prio_hi : 0), DF_EHIP);
     HIP_OR(hipStreamCreateWithPriority(&h->rng_stream, hipStreamNonBlocking, use_prio ? prio_lo : 0), DF_EHIP);
+    HIP_OR(hipStreamCreateWithFlags(&h->ystream, hipStreamNonBlocking), DF_EHIP);
     // The two streams' per-call hand-offs (noise ready, noise set free) order kernels on this GPU and
     // are never waited on by the host (df_sync synchronizes the streams themselves), so they are
     // recorded without the system-scope fence: the reference's grid -2.2%, c2 -1.5% (packed) /
@@ -1299,6 +1368,7 @@ int open_device(df_handle *h, int device)
     for (int set = 0; set < 2; ++set) {
         HIP_OR(hipEventCreateWithFlags(&h->ev_rng[set], ev_flags), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], ev_flags), DF_EHIP);
+        HIP_OR(hipEventCreateWithFlags(&h->ev_swept[set], ev_flags), DF_EHIP);
     }
     return DF_OK;
 }
@@ -1818,6 +1888,10 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->look = 2;
     if (h->hb > 1) h->look = 1;
     if (h->look == 2) h->nsets = std::max(h->nsets, 4);
+    // ...and their y-pass ahead: the next call's y-pass fills the SIMDs while the stream waits on the halo
+    // exchange (one c4/8 rank with a 40 us stand-in exchange: 0.244 / 0.238 -> 0.215 / 0.210 ms, ranks 0 / 4;
+    // 0.196-0.198 either way without it; profiles/r5/d/strip.jsonl)
+    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->yahead = 1;
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -1839,7 +1913,7 @@ int step0(df_handle *h)
     int rc;
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
-    if ((rc = phase_ypass(h, 7))) return rc;
+    if (!h->cur_swept && (rc = phase_ypass(h, 7))) return rc;
     if ((rc = phase_halo_zpass(h, false, false, 0.0))) return rc;
     if ((rc = prefetch_gen(h))) return rc;
     if ((rc = sync_all(h))) return rc;
@@ -1853,9 +1927,12 @@ void destroy(df_handle *h)
     // an unpack or the edge z-pass when a call failed part-way (phase_halo_zpass's error returns).
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
+    if (h->ystream) (void)hipStreamSynchronize(h->ystream);
     if (h->comm_stream) (void)hipStreamSynchronize(h->comm_stream);
     for (auto &pe : h->ev)
         for (auto &e : pe.e) (void)hipEventDestroy(e);
+    for (auto &ye : h->yev)
+        for (auto &e : ye.e) (void)hipEventDestroy(e);
     for (void *p : h->allocs) {
         registry_release(p); // before the free: another thread's hipMalloc may get the address back at once
         (void)hipFree(p);
@@ -1868,8 +1945,10 @@ void destroy(df_handle *h)
     for (int set = 0; set < 2; ++set) {
         if (h->ev_rng[set]) (void)hipEventDestroy(h->ev_rng[set]);
         if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
+        if (h->ev_swept[set]) (void)hipEventDestroy(h->ev_swept[set]);
     }
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    if (h->ystream) (void)hipStreamDestroy(h->ystream);
     if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
     if (h->ev_packed) (void)hipEventDestroy(h->ev_packed);
     if (h->ev_xchg) (void)hipEventDestroy(h->ev_xchg);
@@ -1894,7 +1973,7 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         HIP_OR(hipSetDevice(h->device), DF_EHIP);
         if ((rc = check_rng_error(h))) return rc;
         if ((rc = consume_gen(h))) return rc;
-        if ((rc = phase_ypass(h, 7))) return rc;
+        if (!h->cur_swept && (rc = phase_ypass(h, 7))) return rc;
         if (!h->ghost && (rc = phase_halo_pack(h))) return rc;
     }
     const bool ghost = hs[0]->ghost != 0;
@@ -2039,7 +2118,8 @@ int df_filter(df_handle *h, double dt)
     if ((rc = consume_gen(h))) return rc;
     if ((rc = fused_gen_begin(h))) return rc;
     ev_record(h, 0);
-    if ((rc = phase_ypass(h, 7))) return rc;
+    if (prof) h->ev[h->ev_used].ahead = h->cur_swept;
+    if (!h->cur_swept && (rc = phase_ypass(h, 7))) return rc;
     ev_record(h, 1);
     if ((rc = phase_halo_zpass(h, true, true, dt))) return rc; // phase event 2 inside
     ev_record(h, 3);
@@ -2371,7 +2451,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit},
+        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2399,6 +2479,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = h->ynt_stores = h->geom.nt_stores = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
+    else if (k == "ypass_ahead") h->yahead = value != 0; // from the next epoch generated on (ep_swept)
     else if (k == "zstage") h->zstage = value ? 2 : 0; // 0: the unstaged table z-pass that large halos take (tests)
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
@@ -2536,6 +2617,9 @@ int df_set_profiling(df_handle *h, int on)
         h->ev.resize(1024);
         for (auto &pe : h->ev)
             for (auto &e : pe.e) HIP_OR(hipEventCreate(&e), DF_EHIP);
+        h->yev.resize(256);
+        for (auto &ye : h->yev)
+            for (auto &e : ye.e) HIP_OR(hipEventCreate(&e), DF_EHIP);
     }
     if (on < 0) return fail(DF_EINVAL, "df_set_profiling: on must be >= 0");
     int rc = drain_profile(h);
@@ -2545,6 +2629,9 @@ int df_set_profiling(df_handle *h, int on)
     h->prof = df_profile{};
     h->prof_rng_span = 0;
     h->prof_rng_gens = 0;
+    h->yev_seq = 0;
+    h->prof_y_span = h->prof_y_main = 0;
+    h->prof_y_n = h->prof_y_calls = 0;
     return rc;
 }
 

@@ -310,7 +310,7 @@ def test_runtime_tuning_is_bitexact(mode):
     spec = (131, 260, 2, 16)
     a = gpu_synth(*spec, seed=5, coeff_mode=mode)
     b = gpu_synth(*spec, seed=5, coeff_mode=mode)
-    settings = [dict(rows_per_wave=1, yunroll=4), dict(rows_per_wave=8),
+    settings = [dict(ypass_ahead=1), dict(rows_per_wave=1, yunroll=4), dict(rows_per_wave=8),
                 dict(rows_per_wave=2, yunroll=2, nt_stores=1), dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8),
                 dict(rows_per_wave=4, yunroll=8), dict(gen_split=1), dict(gen_split=4), dict(gen_split=16),
                 dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256), dict(ywin_T=0, zwin_T=4096, zwin_W=0),
@@ -320,7 +320,7 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
-                dict(ylds=1, rows_per_wave=8), dict(ylds=0)]
+                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1)]
     if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back
         settings += [dict(ylds=3, yt_rows=1), dict(yt_rows=2), dict(yt_chunk=8), dict(yt_rows=1, yt_pd=4), dict(yt_pd=2),
                      dict(yt_rows=2, yt_chunk=16), dict(ylds=2), dict(ylds=0)]

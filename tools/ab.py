@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--events", type=int, default=1, help="0: wall time only (no per-call phase events)")
+    ap.add_argument("--switch-calls", type=int, default=1,
+                    help="untimed calls after a --tune switch (a pipeline form takes effect an epoch later)")
     a = ap.parse_args()
     tune = None
     if a.tune_a is not None or a.tune_b is not None:
@@ -83,7 +85,8 @@ def main():
             if tune is not None:
                 for key, val in tune[k]:
                     f.set_tuning(key, val)
-                f.filter(1e-8)  # first call after a switch is not timed
+                for _ in range(a.switch_calls):
+                    f.filter(1e-8)  # calls right after a switch are not timed
             f.set_profiling(bool(a.events))
             f.sync()
             t0 = time.perf_counter()

@@ -1358,7 +1358,6 @@ int open_device(df_handle *h, int device)
     const int use_prio = 0; // measured: priorities cost 1-2% wall time (in-process A/B, tools/ab.py)
     HIP_OR(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, use_prio ? prio_hi : 0), DF_EHIP);
     HIP_OR(hipStreamCreateWithPriority(&h->rng_stream, hipStreamNonBlocking, use_prio ? prio_lo : 0), DF_EHIP);
-    HIP_OR(hipStreamCreateWithFlags(&h->ystream, hipStreamNonBlocking), DF_EHIP);
     // The two streams' per-call hand-offs (noise ready, noise set free) order kernels on this GPU and
     // are never waited on by the host (df_sync synchronizes the streams themselves), so they are
     // recorded without the system-scope fence: the reference's grid -2.2%, c2 -1.5% (packed) /
@@ -1370,6 +1369,18 @@ int open_device(df_handle *h, int device)
         HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], ev_flags), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_swept[set], ev_flags), DF_EHIP);
     }
+    return DF_OK;
+}
+
+// ystream exists only on handles that run the y-pass ahead: a process's streams share the device's few hardware
+// queues (GPU_MAX_HW_QUEUES, 4 here), and a third stream on every handle put the stream and rng_stream of a second
+// live handle on one queue, serialising its noise generation with its sweeps (c3 table 0.341 -> 0.380 ms on the
+// bench line, where the packed handle stays open beside it; profiles/r5/e)
+int ensure_ystream(df_handle *h)
+{
+    if (h->ystream || !h->yahead || h->device < 0) return DF_OK;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipStreamCreateWithFlags(&h->ystream, hipStreamNonBlocking), DF_EHIP);
     return DF_OK;
 }
 
@@ -1897,6 +1908,7 @@ int build(df_handle *h, const df_config_c *cfg)
         return DF_OK;
     }
     if ((rc = open_device(h, cfg->device))) return rc;
+    if ((rc = ensure_ystream(h))) return rc;
     if ((rc = upload_tables(h))) return rc;
     if ((rc = alloc_components(h))) return rc;
     if ((rc = alloc_rng(h, cfg))) return rc;
@@ -2479,7 +2491,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "yunroll") h->yunroll = value >= 8 ? 8 : value >= 4 ? 4 : 2;
     else if (k == "nt_stores") h->nt_stores = h->ynt_stores = h->geom.nt_stores = value != 0;
     else if (k == "zsplit") h->zsplit = value != 0;
-    else if (k == "ypass_ahead") h->yahead = value != 0; // from the next epoch generated on (ep_swept)
+    else if (k == "ypass_ahead") { // from the next epoch generated on (ep_swept)
+        h->yahead = value != 0;
+        if (int rc = ensure_ystream(h)) return rc;
+    }
     else if (k == "zstage") h->zstage = value ? 2 : 0; // 0: the unstaged table z-pass that large halos take (tests)
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)

@@ -81,7 +81,7 @@ struct CompDev {
     long long by_elems = 0, bz_elems = 0; // strip-tap-major element counts
     long long by_size = 0, bz_size = 0;   // reference offset-packed sizes (this strip's cells)
     int ycoop2_xcd[9] = {};               // row-pair y-pass tiles of XCD x: [ycoop2_xcd[x], ycoop2_xcd[x+1])
-    int *ycoop2_perm = nullptr;           // row-pair y-pass: dispatch position -> tile (within each XCD run)
+    int *ycoop2_perm = nullptr;           // row-pair y-pass: dispatch position -> item code (balance_ycoop2)
     double sa = 0, s1a = 0;
 };
 
@@ -109,7 +109,7 @@ struct df_handle {
     int device = 0;
     hipStream_t stream = nullptr;     // sweeps (memory-bound)
     hipStream_t rng_stream = nullptr; // noise generation for the NEXT call (compute-bound), overlapped
-    hipEvent_t ev_rng[2] = {}, ev_release[2] = {};
+    hipEvent_t ev_rng[2] = {}, ev_release[kMaxNoiseSets] = {}; // release: one per epoch slot (epoch_slots)
     // Y-pass ahead (round 5): the y-pass reads only its generation's r_ys and writes only that set's r_zs
     // interior, and depends on nothing a call changes, so it runs on ystream as soon as its epoch's noise is
     // ready, calls ahead of the call that consumes it; the stream then waits for ev_swept instead of ev_rng and
@@ -142,6 +142,8 @@ struct df_handle {
     int ycoop_ovh = 0; // row-pair y-pass: per-tile cost in full-strip taps when balancing the XCD runs
     int ycoop_order = 0; // row-pair y-pass dispatch order within an XCD run: 0 ascending rows, g >= 1 groups of g
                          // consecutive tiles, heaviest group first (balance_ycoop2)
+    int ycoop_split = 0; // row-pair y-pass: tiles whose widest row has N >= ycoop_split run as two 64-column halves
+                         // (two blocks, each half the chunks of the tile's chain); 0 = never
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
     std::vector<int> ycoop2_perm_host[3]; // balance_ycoop2's dispatch order (uploaded to CompDev::ycoop2_perm)
     // z-strips: 1 = every rank counts every attempt block, so the halo send/recv is the call's only
@@ -386,7 +388,7 @@ SweepArgs sweep_args(df_handle *h)
         }
     for (int c = 0; c < 3; ++c) {
         a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
-        a.ycoop2_perm[c] = h->ycoop_order ? h->c[c].ycoop2_perm : nullptr;
+        a.ycoop2_perm[c] = h->ycoop_order || h->ycoop_split ? h->c[c].ycoop2_perm : nullptr;
     }
     a.ylds = h->ylds;
     a.ylist = h->ylist;
@@ -522,6 +524,9 @@ constexpr int kHbRestoreCalls = 16;
 long long gen_epoch(const df_handle *h, long long g) { return h->hb == 1 ? g : (g - h->gen_base) / h->hb; }
 int gen_pos(const df_handle *h, long long g) { return h->hb == 1 ? 0 : (int)((g - h->gen_base) % h->hb); }
 int gen_set(const df_handle *h, long long g) { return (int)(g % h->nsets); }
+// Epochs whose noise sets the handle holds at once (nsets / hb): epoch e reuses epoch e - slots' sets, free once
+// epoch e - slots + 1 has begun (ev_release[(e - slots) % slots], recorded then on the stream)
+int epoch_slots(const df_handle *h) { return h->nsets / h->hb; }
 
 // Noise pipeline. The reference draws all six noise arrays at the start of each
 // call (df.cpp:453); the draws depend only on the stream state, so generation n+1
@@ -540,9 +545,9 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
     const long long gi = h->gen_launched, e = gen_epoch(h, gi);
     const int set = gen_set(h, gi);
     rs = h->overlap ? h->rng_stream : h->stream;
-    // the epoch's sets were last read by epoch e - 2 (2*hb sets), released when epoch e - 1 began
-    if (gen_pos(h, gi) == 0 && (h->hb == 1 || e >= 2))
-        HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e & 1], 0), DF_EHIP);
+    // the epoch's sets were last read by epoch e - K (K = epoch_slots), released when epoch e - K + 1 began
+    const int K = epoch_slots(h);
+    if (gen_pos(h, gi) == 0 && e >= K) HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e % K], 0), DF_EHIP);
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
@@ -712,7 +717,7 @@ int consume_gen(df_handle *h)
     const bool first = gen_pos(h, gi) == 0;
     int rc;
     if (first && gi > (h->hb == 1 ? 0 : h->gen_base))
-        HIP_OR(hipEventRecord(h->ev_release[(e - 1) & 1], h->stream), DF_EHIP); // the previous epoch's sets free
+        HIP_OR(hipEventRecord(h->ev_release[(e - 1) % epoch_slots(h)], h->stream), DF_EHIP); // the previous epoch's sets free
     const long long need = h->hb == 1 ? gi + 1 : h->gen_base + (e + 1) * h->hb; // this epoch, launched
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
@@ -735,7 +740,10 @@ int prefetch_gen(df_handle *h)
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
     (void)gi;
-    const long long need = h->gen_used + (fused_active(h) ? h->look : h->hb);
+    // ahead handles hold three epochs of sets (consumed, swept, generating): generation two epochs on, so an
+    // epoch's y-passes never wait for its own generation to start behind the release of the epoch before
+    const int depth = h->yahead && h->ystream && epoch_slots(h) >= 3 ? 2 : 1;
+    const long long need = h->gen_used + (fused_active(h) ? h->look : depth * h->hb);
     int rc;
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
@@ -1065,6 +1073,11 @@ int read_config(df_handle *h, const df_config_c *cfg)
 // strip (the reference's grid: N_y 28-212 along the rows, a 16-column last strip) and leaves them idle
 // while the others stream. Cost of a tile = its coefficient taps x live columns + ycoop_ovh full-strip
 // taps (a per-block fixed cost).
+// Work items: a tile, or (ycoop_split) one 64-column half of a wide-stencil tile. A block's chunks are its chain
+// of dependent round trips, and every resident block gets about the same share of HBM, so a 27-chunk tile of the
+// reference's grid ends the launch long after the 4-chunk ones; its halves fold two tap groups into each wave
+// (as the narrow last strip does), so each walks the chain in half the chunks, in parallel. Code = tile * 4 +
+// part (0 whole, 1 columns 0-63, 2 columns 64-127).
 void balance_ycoop2(df_handle *h, int c)
 {
     constexpr int RR = 2; // rows per block of the row-pair y-pass
@@ -1072,15 +1085,30 @@ void balance_ycoop2(df_handle *h, int c)
     const std::vector<int> &Nst = h->y_nst[c];
     // host-only handles (no device state) never built the tap ranges: nothing to balance
     if (Nst.size() < (size_t)h->nstrips * Ny) return;
-    std::vector<double> wgt((size_t)h->nstrips * nrb);
+    std::vector<double> wgt;
+    std::vector<int> code;
     const double ovh = (double)h->ycoop_ovh * kStrip;
     double tot = 0;
     for (int st = 0; st < h->nstrips; ++st) {
         const int live = std::min(kStrip, h->Nz_loc - st * kStrip);
         for (int rb = 0; rb < nrb; ++rb) {
             double taps = 0;
-            for (int j = rb * RR; j < std::min(Ny, rb * RR + RR); ++j) taps += 2 * Nst[(size_t)st * Ny + j] + 1;
-            tot += wgt[(size_t)st * nrb + rb] = taps * live + ovh;
+            int nmax = 0;
+            for (int j = rb * RR; j < std::min(Ny, rb * RR + RR); ++j) {
+                taps += 2 * Nst[(size_t)st * Ny + j] + 1;
+                nmax = std::max(nmax, Nst[(size_t)st * Ny + j]);
+            }
+            const int tile = st * nrb + rb;
+            if (h->ycoop_split > 0 && live > 64 && nmax >= h->ycoop_split) {
+                for (int part = 1; part <= 2; ++part) {
+                    wgt.push_back(taps * (part == 1 ? 64 : live - 64) + ovh);
+                    code.push_back(tile * 4 + part);
+                }
+            } else {
+                wgt.push_back(taps * live + ovh);
+                code.push_back(tile * 4);
+            }
+            tot += taps * live + ovh;
         }
     }
     int *xr = h->c[c].ycoop2_xcd;
@@ -1095,14 +1123,13 @@ void balance_ycoop2(df_handle *h, int c)
     // Dispatch order inside each XCD run. Ascending rows (order 0) keeps neighbouring row pairs, which share
     // most noise rows, resident together; but where the widest stencils sit at the end of a run (the
     // reference's grid: N_y peaks at 212 around j = 170, N 28-60 elsewhere) they start last and the run
-    // ends on a tail of 27-chunk blocks. Order g >= 1: groups of g consecutive tiles, heaviest group first.
-    h->ycoop2_perm_host[c].assign(wgt.size(), 0);
+    // ends on a tail of 27-chunk blocks. Order g >= 1: groups of g consecutive items, heaviest group first.
     std::vector<int> &perm = h->ycoop2_perm_host[c];
-    for (size_t t = 0; t < perm.size(); ++t) perm[t] = (int)t;
+    perm = code;
     const int gsz = h->ycoop_order;
     if (gsz > 0)
         for (int xx = 0; xx < 8; ++xx) {
-            std::vector<std::pair<double, int>> grp; // (group weight, first tile)
+            std::vector<std::pair<double, int>> grp; // (group weight, first item)
             for (int t = xr[xx]; t < xr[xx + 1]; t += gsz) {
                 double w = 0;
                 for (int u = t; u < std::min(t + gsz, xr[xx + 1]); ++u) w += wgt[u];
@@ -1111,7 +1138,7 @@ void balance_ycoop2(df_handle *h, int c)
             std::stable_sort(grp.begin(), grp.end(), [](const auto &p, const auto &q) { return p.first > q.first; });
             int pos = xr[xx];
             for (const auto &gq : grp)
-                for (int u = gq.second; u < std::min(gq.second + gsz, xr[xx + 1]); ++u) perm[pos++] = u;
+                for (int u = gq.second; u < std::min(gq.second + gsz, xr[xx + 1]); ++u) perm[pos++] = code[u];
         }
 }
 
@@ -1208,6 +1235,10 @@ int plan_strips(df_handle *h)
         if (h->coeff_mode == DF_COEFF_PACKED && long_chain) {
             h->ycoop = 7;
             h->ycoop_order = 4;
+            // tiles whose widest row has N >= 96 run as two 64-column halves (balance_ycoop2): the reference's
+            // grid y-pass 149 -> 146 us alone, call -1% (serial) / -4% (y-pass ahead); thresholds 64-160 within
+            // 1% of each other (profiles/r5/g)
+            h->ycoop_split = 96;
         }
         // Long chains, both modes: the y-pass runs ahead on its own stream (df_handle::yahead), so a call's
         // z-pass shares the chip with later calls' y-passes instead of idling beside its own latency-bound tail
@@ -1366,9 +1397,9 @@ int open_device(df_handle *h, int device)
     const unsigned ev_flags = hipEventDisableTiming | hipEventDisableSystemFence;
     for (int set = 0; set < 2; ++set) {
         HIP_OR(hipEventCreateWithFlags(&h->ev_rng[set], ev_flags), DF_EHIP);
-        HIP_OR(hipEventCreateWithFlags(&h->ev_release[set], ev_flags), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_swept[set], ev_flags), DF_EHIP);
     }
+    for (int k = 0; k < kMaxNoiseSets; ++k) HIP_OR(hipEventCreateWithFlags(&h->ev_release[k], ev_flags), DF_EHIP);
     return DF_OK;
 }
 
@@ -1376,6 +1407,19 @@ int open_device(df_handle *h, int device)
 // queues (GPU_MAX_HW_QUEUES, 4 here), and a third stream on every handle put the stream and rng_stream of a second
 // live handle on one queue, serialising its noise generation with its sweeps (c3 table 0.341 -> 0.380 ms on the
 // bench line, where the packed handle stays open beside it; profiles/r5/e)
+// comm_stream (high priority) exists only where the halo overlap form can run: packed z-strips by default, table
+// ones once halo_overlap is set to 1 - the streams of a process share the device's hardware queues (above)
+int ensure_comm_stream(df_handle *h)
+{
+    const bool ov = h->halo_overlap > 0 || (h->halo_overlap < 0 && h->coeff_mode == DF_COEFF_PACKED);
+    if (h->comm_stream || !ov || h->device < 0 || h->world < 2 || !(h->comm || h->solo_strip)) return DF_OK;
+    int prio_lo = 0, prio_hi = 0;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
+    HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
+    return DF_OK;
+}
+
 int ensure_ystream(df_handle *h)
 {
     if (h->ystream || !h->yahead || h->device < 0) return DF_OK;
@@ -1487,7 +1531,7 @@ int alloc_components(df_handle *h)
                 }
         }
         h->y_nst[c] = Nst[0]; // host copy for the row-block y-pass's XCD balance
-        if ((rc = dalloc_t(h, &d.ycoop2_perm, (size_t)h->nstrips * ((Ny + 1) / 2)))) return rc;
+        if ((rc = dalloc_t(h, &d.ycoop2_perm, 2 * (size_t)h->nstrips * ((Ny + 1) / 2)))) return rc; // halves
         balance_ycoop2(h, c);
         if ((rc = upload_ycoop2_perm(h, c))) return rc;
         if ((rc = dalloc_t(h, &d.Ny_st, Nst[0].size()))) return rc;
@@ -1850,9 +1894,7 @@ int open_comm(df_handle *h, const df_config_c *cfg)
         h->split_count = !h->rng_replicate;
     }
     if (h->world > 1 && (cfg->comm_id || h->solo_strip)) {
-        int prio_lo = 0, prio_hi = 0;
-        HIP_OR(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi), DF_EHIP);
-        HIP_OR(hipStreamCreateWithPriority(&h->comm_stream, hipStreamNonBlocking, prio_hi), DF_EHIP);
+        if (int rc2 = ensure_comm_stream(h)) return rc2;
         HIP_OR(hipEventCreateWithFlags(&h->ev_packed, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_xchg, hipEventDisableTiming), DF_EHIP);
         HIP_OR(hipEventCreateWithFlags(&h->ev_unpacked, hipEventDisableTiming), DF_EHIP);
@@ -1890,8 +1932,14 @@ int build(df_handle *h, const df_config_c *cfg)
     }
     if (h->hb != 1 && h->hb != 2 && h->hb != 4) return fail(DF_EINVAL, "handoff batch must be 1, 2 or 4");
     if (h->world > 1 || cfg->comm_id) h->hb = 1;
+    // RCCL table z-strips run the y-pass ahead: the next call's y-pass fills the SIMDs while the stream waits on
+    // the halo exchange (one c4/8 rank with a 40 us stand-in exchange: 0.244 / 0.238 -> 0.215 / 0.210 ms, ranks
+    // 0 / 4; 0.196-0.198 either way without it; profiles/r5/d/strip.jsonl)
+    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->yahead = 1;
+    // ahead handles hold three epochs of noise sets (consumed, swept ahead, generating)
     h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
+    if (h->yahead) h->nsets = 3 * h->hb;
     // z-strip handles in table mode, one process per GPU (split counting, the fused exchange): generations two
     // calls ahead. look is consulted only by fused_active() handles (one generation per hand-off), so in-process
     // groups and batched handles keep look 1 and the noise sets their batch needs (a batched handle
@@ -1899,10 +1947,6 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->look = 2;
     if (h->hb > 1) h->look = 1;
     if (h->look == 2) h->nsets = std::max(h->nsets, 4);
-    // ...and their y-pass ahead: the next call's y-pass fills the SIMDs while the stream waits on the halo
-    // exchange (one c4/8 rank with a 40 us stand-in exchange: 0.244 / 0.238 -> 0.215 / 0.210 ms, ranks 0 / 4;
-    // 0.196-0.198 either way without it; profiles/r5/d/strip.jsonl)
-    if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->yahead = 1;
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -1914,7 +1958,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if ((rc = alloc_rng(h, cfg))) return rc;
     if (h->gen_dense == 2 && h->geom.gen_split == 1 && (rc = alloc_dense(h))) return rc;
     if ((rc = open_comm(h, cfg))) return rc;
-    for (int set = 0; set < 2; ++set) HIP_OR(hipEventRecord(h->ev_release[set], h->stream), DF_EHIP);
+    for (int k = 0; k < kMaxNoiseSets; ++k) HIP_OR(hipEventRecord(h->ev_release[k], h->stream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     return DF_OK;
 }
@@ -1956,9 +2000,10 @@ void destroy(df_handle *h)
     if (h->ev_halo) (void)hipEventDestroy(h->ev_halo);
     for (int set = 0; set < 2; ++set) {
         if (h->ev_rng[set]) (void)hipEventDestroy(h->ev_rng[set]);
-        if (h->ev_release[set]) (void)hipEventDestroy(h->ev_release[set]);
         if (h->ev_swept[set]) (void)hipEventDestroy(h->ev_swept[set]);
     }
+    for (int k = 0; k < kMaxNoiseSets; ++k)
+        if (h->ev_release[k]) (void)hipEventDestroy(h->ev_release[k]);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->ystream) (void)hipStreamDestroy(h->ystream);
     if (h->comm_stream) (void)hipStreamDestroy(h->comm_stream);
@@ -2463,7 +2508,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
+        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2544,11 +2589,12 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a call in flight keeps the form it was enqueued with
         h->halo_overlap = value < 0 ? -1 : value != 0;
+        if (int rc = ensure_comm_stream(h)) return rc;
     }
 
-    else if (k == "ycoop_order") {
-        if (value < 0) return fail(DF_EINVAL, "ycoop_order must be >= 0");
-        h->ycoop_order = value;
+    else if (k == "ycoop_order" || k == "ycoop_split") {
+        if (value < 0) return fail(DF_EINVAL, k + " must be >= 0");
+        (k == "ycoop_order" ? h->ycoop_order : h->ycoop_split) = value;
         if (valid_dev(h)) {
             if (int rc = sync_all(h)) return rc;
             for (int c = 0; c < 3; ++c) {
@@ -2580,7 +2626,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
-        if (value > 1 && 2 * value > h->nsets)
+        if (value > 1 && (2 * value > h->nsets || h->nsets % value))
             return fail(DF_EINVAL, "handoff_batch " + std::to_string(value) + " needs " + std::to_string(2 * value) +
                                        " noise sets; this handle has " + std::to_string(h->nsets) +
                                        " (DFAMD_HANDOFF_BATCH at create)");

@@ -1529,12 +1529,15 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     const int x = blockIdx.x & 7;
     const int pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
     if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
-    const int tile = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos;
+    const int code = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos * 4; // tile * 4 + part (balance_ycoop2)
+    const int tile = code >> 2, part = code & 3;
     const int s = tile / nrowblk;             // rows ascending within a strip (L2 reuse of noise rows)
     const int j0 = (tile - s * nrowblk) * RR;
     const int nr = min(RR, Ny - j0);
-    // live column pairs of this strip -> P lanes per tap group (power of two), G groups per wave
-    const int pairs = min(kStrip / 2, (a.Nz_loc - s * kStrip + 1) >> 1);
+    // the item's columns: the whole strip, or one 64-column half of it (part 1, 2)
+    const int cb = part == 2 ? 64 : 0, c0 = s * kStrip + cb;
+    // live column pairs of this item -> P lanes per tap group (power of two), G groups per wave
+    const int pairs = min(part ? 32 : kStrip / 2, (a.Nz_loc - c0 + 1) >> 1);
     int lp = 0;
     while ((1 << lp) < pairs) ++lp;
     const int P = 1 << lp, G = 64 >> lp, CHG = CH * G;
@@ -1550,10 +1553,10 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
         hi[r] = j0 + rr + N;
         mlo = min(mlo, lo[r]);
         mhi = max(mhi, hi[r]);
-        bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + rr] + 2 * p; // tap t at bp + t*128
+        bp[r] = a.By[c] + a.byoff[c][(size_t)s * Ny + j0 + rr] + cb + 2 * p; // tap t at bp + t*128
     }
     const int M = mhi - mlo + 1;
-    const int col = s * kStrip + 2 * p;
+    const int col = c0 + 2 * p;
     const bool live = col < a.Nz_loc;
     const double *np = a.ry[c] + (size_t)(mlo + a.Nyp[c]) * a.Pz + col; // noise row mlo + u at np + u*Pz
     double2 b[RR][KPW], n[KPW];
@@ -1624,7 +1627,7 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
         }
         __syncthreads();
     }
-    const int k = s * kStrip + cell;
+    const int k = c0 + cell;
 #pragma unroll
     for (int i = 0; i < RH; ++i) {
         const int r = 2 * i + rs;

@@ -23,7 +23,7 @@
 namespace dfamd {
 
 constexpr int kStrip = 128;           // cells per strip (one wave, 2 per lane)
-constexpr int kMaxNoiseSets = 8;      // noise sets per handle (2 x the hand-off batch, <= 4)
+constexpr int kMaxNoiseSets = 12;     // noise sets per handle (2 x the hand-off batch; 3 x with the y-pass ahead)
 constexpr int kRngThreads = 256;      // threads per RNG block
 constexpr int kRngPerThread = 16;     // polar attempts per thread
 constexpr int kRngBlockAttempts = kRngThreads * kRngPerThread;

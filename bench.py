@@ -682,6 +682,14 @@ def summarize(ctx, wl, args, recs):
     if ctx.world > 1:
         out["roofline"] = dict(slowest["roofline"], rank=slowest["rank"],
                                frac_by_rank=[r["roofline"]["frac"] for r in recs])
+    if args.coeff_mode == "packed" and all(r.get("call_bytes") for r in recs):
+        # the whole call's algorithmic bytes (y- and z-pass) over the wall per call: where the y-pass
+        # runs ahead it shares the chip with the z-pass, and the kernel figure above counts only its own bytes
+        cb = sum(r["call_bytes"] for r in recs)
+        gbs = cb / (ms * 1e-3) / 1e9
+        out["roofline"] = dict(out["roofline"], call={
+            "bytes": cb, "ms": round(ms, 4), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBPS, 4),
+            "note": "every sweep's algorithmic bytes of one call / ms_per_step (all ranks)"})
         cm = recs[0]["comm"] or {}
         out["multi_gpu"] = {
             "rccl_ranks": cm.get("rccl_ranks"),

@@ -18,7 +18,7 @@ def main():
     for n, o in (d.get("other_configs") or {}).items():
         rf = o.get("roofline") or o.get("roofline_valu") or {}
         print(f"  {n}: ms={o['ms_per_step']} parity_ok={o.get('parity_ok')} frac={rf.get('frac')} "
-              f"traffic={rf.get('traffic')}"
+              f"traffic={rf.get('traffic')} call_frac={(rf.get('call') or {}).get('frac')}"
               + (f" cpu_ref={o['cpu_reference']}" if 'cpu_reference' in o else "")
               + (f" same_plane={o['same_plane_1gpu']['ms_per_step']}" if o.get('same_plane_1gpu') else "")
               + (f" long_run={ {k: o['long_run'][k] for k in ('steps', 'total_s', 'steady_ms_per_call')} }"

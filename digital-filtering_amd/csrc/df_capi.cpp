@@ -2627,9 +2627,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
         if (value > 1 && (2 * value > h->nsets || h->nsets % value))
-            return fail(DF_EINVAL, "handoff_batch " + std::to_string(value) + " needs " + std::to_string(2 * value) +
-                                       " noise sets; this handle has " + std::to_string(h->nsets) +
-                                       " (DFAMD_HANDOFF_BATCH at create)");
+            return fail(DF_EINVAL, "handoff_batch " + std::to_string(value) + " needs at least " +
+                                       std::to_string(2 * value) + " noise sets, a multiple of it; this handle has " +
+                                       std::to_string(h->nsets) + " (sized at create by the plane's own batch)");
         if (value > 1 && (h->world > 1 || h->comm || h->group))
             return fail(DF_EINVAL, "handoff_batch > 1 is for single-GPU handles");
         h->hb_conf = value;

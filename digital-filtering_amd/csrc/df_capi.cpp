@@ -1242,8 +1242,9 @@ int plan_strips(df_handle *h)
         }
         // Long chains, both modes: the y-pass runs ahead on its own stream (df_handle::yahead), so a call's
         // z-pass shares the chip with later calls' y-passes instead of idling beside its own latency-bound tail
-        // (same handle A/B, 9 rounds: the reference's grid packed 0.194 -> 0.165 ms, table 0.060 -> 0.055;
-        // c1 even; HBM-bound c2 +9%, c3 +0.6..1%: two streaming passes at once only contend; profiles/r5/d)
+        // (same-handle A/B in steady state: the reference's grid packed 0.168 -> 0.141 ms, table 0.0423 -> 0.0419;
+        // c3 table +0.8%, c2 -1% packed / +9% table, c1 +5..7%: two streaming passes at once, or a launch-bound
+        // call, only contend; profiles/r5/h, i)
         if (long_chain) h->yahead = 1;
         // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
         // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;

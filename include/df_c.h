@@ -216,7 +216,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   g >= 1 groups of g tiles heaviest first; 4 on long chains), "ycoop_split" (row-pair tiles whose widest
  *   row has N >= this run as two 64-column halves; 96 on long chains, 0 never), "ypass_ahead" (1: each
  *   epoch's y-passes run on a stream of their own as soon as its noise is generated and the call runs only
- *   the halo and z-pass; long-chain planes and RCCL table z-strips), "ylds" (table y-pass with LDS-staged noise:
+ *   the halo and z-pass; long-chain planes and RCCL table z-strips; it pays only with the three epochs of noise
+ *   sets such handles allocate at create), "ylds" (table y-pass with LDS-staged noise:
  *   2 = a block per (strip, 4 rows), 3 = a block per (64 columns, 4 waves of "yt_rows" rows) walking the
  *   tap window in "yt_chunk"-row chunks through a double-buffered LDS ring, "yt_pd" chunks of noise loads
  *   in flight, heaviest first; 0 = a wave per tile), "yt_rows" x "yt_chunk" (1 x 16 default, 2 x 8,

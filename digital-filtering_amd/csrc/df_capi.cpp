@@ -144,6 +144,7 @@ struct df_handle {
                          // consecutive tiles, heaviest group first (balance_ycoop2)
     int ycoop_split = 0; // row-pair y-pass: tiles whose widest row has N >= ycoop_split run as two 64-column halves
                          // (two blocks, each half the chunks of the tile's chain); 0 = never
+    int ycoop_split4 = 0; // ... and those with N >= ycoop_split4 as four 32-column quarters; 0 = never
     std::vector<int> y_nst[3]; // host copy of Ny_st (tap range per strip and row) for balance_ycoop2
     std::vector<int> ycoop2_perm_host[3]; // balance_ycoop2's dispatch order (uploaded to CompDev::ycoop2_perm)
     // z-strips: 1 = every rank counts every attempt block, so the halo send/recv is the call's only
@@ -388,7 +389,7 @@ SweepArgs sweep_args(df_handle *h)
         }
     for (int c = 0; c < 3; ++c) {
         a.ycoop2_xcd[c][8] = h->c[c].ycoop2_xcd[8];
-        a.ycoop2_perm[c] = h->ycoop_order || h->ycoop_split ? h->c[c].ycoop2_perm : nullptr;
+        a.ycoop2_perm[c] = h->ycoop_order || h->ycoop_split || h->ycoop_split4 ? h->c[c].ycoop2_perm : nullptr;
     }
     a.ylds = h->ylds;
     a.ylist = h->ylist;
@@ -1077,7 +1078,7 @@ int read_config(df_handle *h, const df_config_c *cfg)
 // of dependent round trips, and every resident block gets about the same share of HBM, so a 27-chunk tile of the
 // reference's grid ends the launch long after the 4-chunk ones; its halves fold two tap groups into each wave
 // (as the narrow last strip does), so each walks the chain in half the chunks, in parallel. Code = tile * 4 +
-// part (0 whole, 1 columns 0-63, 2 columns 64-127).
+// part (0 whole, 1-2 the 64-column halves, 3-6 the 32-column quarters; ycoop_split4).
 void balance_ycoop2(df_handle *h, int c)
 {
     constexpr int RR = 2; // rows per block of the row-pair y-pass
@@ -1099,14 +1100,19 @@ void balance_ycoop2(df_handle *h, int c)
                 nmax = std::max(nmax, Nst[(size_t)st * Ny + j]);
             }
             const int tile = st * nrb + rb;
-            if (h->ycoop_split > 0 && live > 64 && nmax >= h->ycoop_split) {
+            if (h->ycoop_split4 > 0 && live == kStrip && nmax >= h->ycoop_split4) {
+                for (int part = 3; part <= 6; ++part) {
+                    wgt.push_back(taps * 32 + ovh);
+                    code.push_back(tile * 8 + part);
+                }
+            } else if (h->ycoop_split > 0 && live > 64 && nmax >= h->ycoop_split) {
                 for (int part = 1; part <= 2; ++part) {
                     wgt.push_back(taps * (part == 1 ? 64 : live - 64) + ovh);
-                    code.push_back(tile * 4 + part);
+                    code.push_back(tile * 8 + part);
                 }
             } else {
                 wgt.push_back(taps * live + ovh);
-                code.push_back(tile * 4);
+                code.push_back(tile * 8);
             }
             tot += taps * live + ovh;
         }
@@ -1235,16 +1241,16 @@ int plan_strips(df_handle *h)
         if (h->coeff_mode == DF_COEFF_PACKED && long_chain) {
             h->ycoop = 7;
             h->ycoop_order = 4;
-            // tiles whose widest row has N >= 96 run as two 64-column halves (balance_ycoop2): the reference's
-            // grid y-pass 149 -> 146 us alone, call -1% (serial) / -4% (y-pass ahead); thresholds 64-160 within
-            // 1% of each other (profiles/r5/g)
+            // tiles whose widest row has N >= 96 run as two 64-column halves, N >= 192 as four 32-column
+            // quarters (balance_ycoop2): the reference's grid call -4.2% and another -0.8% (one-handle A/B,
+            // 60-call windows, both orders; profiles/r5/m; halves at thresholds 64-160 within 1%, r5/g)
             h->ycoop_split = 96;
+            h->ycoop_split4 = 192;
         }
         // Long chains, both modes: the y-pass runs ahead on its own stream (df_handle::yahead), so a call's
         // z-pass shares the chip with later calls' y-passes instead of idling beside its own latency-bound tail
-        // (same-handle A/B in steady state: the reference's grid packed 0.168 -> 0.141 ms, table 0.0423 -> 0.0419;
-        // c3 table +0.8%, c2 -1% packed / +9% table, c1 +5..7%: two streaming passes at once, or a launch-bound
-        // call, only contend; profiles/r5/h, i)
+        // (one-handle A/B with 60-call windows, both orders: the reference's grid packed -0.5%, table -1%; c3
+        // table, c2 and c1 neutral or slower, so off there; profiles/r5/m, i)
         if (long_chain) h->yahead = 1;
         // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
         // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
@@ -1532,7 +1538,7 @@ int alloc_components(df_handle *h)
                 }
         }
         h->y_nst[c] = Nst[0]; // host copy for the row-block y-pass's XCD balance
-        if ((rc = dalloc_t(h, &d.ycoop2_perm, 2 * (size_t)h->nstrips * ((Ny + 1) / 2)))) return rc; // halves
+        if ((rc = dalloc_t(h, &d.ycoop2_perm, 4 * (size_t)h->nstrips * ((Ny + 1) / 2)))) return rc; // quarters
         balance_ycoop2(h, c);
         if ((rc = upload_ycoop2_perm(h, c))) return rc;
         if ((rc = dalloc_t(h, &d.Ny_st, Nst[0].size()))) return rc;
@@ -2509,7 +2515,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
+        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2593,9 +2599,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (int rc = ensure_comm_stream(h)) return rc;
     }
 
-    else if (k == "ycoop_order" || k == "ycoop_split") {
+    else if (k == "ycoop_order" || k == "ycoop_split" || k == "ycoop_split4") {
         if (value < 0) return fail(DF_EINVAL, k + " must be >= 0");
-        (k == "ycoop_order" ? h->ycoop_order : h->ycoop_split) = value;
+        (k == "ycoop_order" ? h->ycoop_order : k == "ycoop_split" ? h->ycoop_split : h->ycoop_split4) = value;
         if (valid_dev(h)) {
             if (int rc = sync_all(h)) return rc;
             for (int c = 0; c < 3; ++c) {

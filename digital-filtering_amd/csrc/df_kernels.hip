@@ -1529,15 +1529,16 @@ __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
     const int x = blockIdx.x & 7;
     const int pos = a.ycoop2_xcd[c][x] + (int)(blockIdx.x >> 3);
     if (pos >= a.ycoop2_xcd[c][x + 1]) return; // block-uniform
-    const int code = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos * 4; // tile * 4 + part (balance_ycoop2)
-    const int tile = code >> 2, part = code & 3;
+    const int code = a.ycoop2_perm[c] ? a.ycoop2_perm[c][pos] : pos * 8; // tile * 8 + part (balance_ycoop2)
+    const int tile = code >> 3, part = code & 7;
     const int s = tile / nrowblk;             // rows ascending within a strip (L2 reuse of noise rows)
     const int j0 = (tile - s * nrowblk) * RR;
     const int nr = min(RR, Ny - j0);
-    // the item's columns: the whole strip, or one 64-column half of it (part 1, 2)
-    const int cb = part == 2 ? 64 : 0, c0 = s * kStrip + cb;
+    // the item's columns: the whole strip (part 0), a 64-column half (1, 2) or a 32-column quarter (3-6)
+    const int iw = part == 0 ? kStrip : part <= 2 ? 64 : 32;
+    const int cb = part == 0 ? 0 : part <= 2 ? (part - 1) * 64 : (part - 3) * 32, c0 = s * kStrip + cb;
     // live column pairs of this item -> P lanes per tap group (power of two), G groups per wave
-    const int pairs = min(part ? 32 : kStrip / 2, (a.Nz_loc - c0 + 1) >> 1);
+    const int pairs = min(iw / 2, (a.Nz_loc - c0 + 1) >> 1);
     int lp = 0;
     while ((1 << lp) < pairs) ++lp;
     const int P = 1 << lp, G = 64 >> lp, CHG = CH * G;

@@ -214,7 +214,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   8-deep load ring of long chains), "ycoop" (packed y-pass: 7 = a block per row pair, the long-chain
  *   default; 0 = a wave per tile), "ycoop_order" (row-pair dispatch inside each XCD run: 0 ascending,
  *   g >= 1 groups of g tiles heaviest first; 4 on long chains), "ycoop_split" (row-pair tiles whose widest
- *   row has N >= this run as two 64-column halves; 96 on long chains, 0 never), "ypass_ahead" (1: each
+ *   row has N >= this run as two 64-column halves; 96 on long chains, 0 never), "ycoop_split4" (... as four
+ *   32-column quarters; 192 on long chains), "ypass_ahead" (1: each
  *   epoch's y-passes run on a stream of their own as soon as its noise is generated and the call runs only
  *   the halo and z-pass; long-chain planes and RCCL table z-strips; it pays only with the three epochs of noise
  *   sets such handles allocate at create), "ylds" (table y-pass with LDS-staged noise:

@@ -188,6 +188,7 @@ def test_golden_native_grid(mode, tuning):
 @pytest.mark.parametrize("mode,tuning", [("packed", {}), ("packed", dict(ycoop=0)), ("packed", dict(ycoop_order=1)),
                                          ("packed", dict(ycoop_order=8)), ("packed", dict(ycoop_split=96)),
                                          ("packed", dict(ycoop_split=1, ycoop_order=0)), ("packed", dict(ycoop_split=0)),
+                                         ("packed", dict(ycoop_split4=160)), ("packed", dict(ycoop_split4=1, ycoop_split=0)),
                                          ("table", {}), ("table", dict(rows_per_wave=1)),
                                          ("table", dict(ylds=1)), ("table", dict(ylds=2, rows_per_wave=2)),
                                          ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
@@ -315,7 +316,7 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(rows_per_wave=2, yunroll=2, nt_stores=1), dict(nt_stores=0), dict(rows_per_wave=1, yunroll=8),
                 dict(rows_per_wave=4, yunroll=8), dict(gen_split=1), dict(gen_split=4), dict(gen_split=16),
                 dict(ywin_T=1024, ywin_W=64, zwin_T=2048, zwin_W=256), dict(ywin_T=0, zwin_T=4096, zwin_W=0),
-                dict(gen_split=2), dict(zsplit=1), dict(zsplit=0), dict(ycoop=7), dict(ycoop=7, ycoop_order=1), dict(ycoop=7, ycoop_order=4), dict(ycoop_split=8), dict(ycoop_order=0), dict(ycoop_split=12), dict(ycoop_split=0),
+                dict(gen_split=2), dict(zsplit=1), dict(zsplit=0), dict(ycoop=7), dict(ycoop=7, ycoop_order=1), dict(ycoop=7, ycoop_order=4), dict(ycoop_split=8), dict(ycoop_order=0), dict(ycoop_split=12), dict(ycoop_split4=10), dict(ycoop_split=0), dict(ycoop_split4=0),
                 dict(ycoop=0, yunroll=2), dict(rows_per_wave=2), dict(rows_per_wave=1), dict(rows_per_wave=8),
                 dict(fuse_plan=0, gen_split=1, gen_dense=2),
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),

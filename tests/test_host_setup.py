@@ -330,8 +330,8 @@ def test_alloc_registry_rejects_overlapping_ranges():
     # the reference's grid (y half-widths up to 212): table LDS-staged 64-column tiles (ypass_t64), epochs of 4;
     # packed the row-pair y-pass in heaviest-first groups of 4; both with the y-pass ahead on its own stream
     (dict(), "table", dict(rows_per_wave=1, ylds=3, yt_rows=1, yt_chunk=16, handoff_batch=4, ycoop=0, ypass_ahead=1)),
-    (dict(), "packed", dict(rows_per_wave=1, ycoop=7, ycoop_order=4, ycoop_split=96, ylds=0, handoff_batch=4,
-                            ypass_ahead=1)),
+    (dict(), "packed", dict(rows_per_wave=1, ycoop=7, ycoop_order=4, ycoop_split=96, ycoop_split4=192, ylds=0,
+                            handoff_batch=4, ypass_ahead=1)),
     # c3 (half-widths 4-64): table 4 rows per wave (ypass_table_kernel), no LDS staging, two generations per
     # hand-off, the run generation; packed 2 rows, one hand-off per call
     (dict(plane="synthetic", Ny=2048, Nz=2048, N_min=4, N_max=64), "table",

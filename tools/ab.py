@@ -62,7 +62,9 @@ def main():
     ap.add_argument("--tune-a", default=None)
     ap.add_argument("--tune-b", default=None)
     ap.add_argument("--rounds", type=int, default=7)
-    ap.add_argument("--calls", type=int, default=10)
+    # 60: pipelines that run ahead (noise epochs, the y-pass ahead) hold several calls of work past a window's
+    # last call; 10-call windows timed the first setting of each round ~40% slower (profiles/r5/m)
+    ap.add_argument("--calls", type=int, default=60)
     ap.add_argument("--events", type=int, default=1, help="0: wall time only (no per-call phase events)")
     ap.add_argument("--switch-calls", type=int, default=1,
                     help="untimed calls after a --tune switch (a pipeline form takes effect an epoch later)")

@@ -1252,10 +1252,12 @@ int plan_strips(df_handle *h)
         // (one-handle A/B with 60-call windows, both orders: the reference's grid packed -0.5%, table -1%; c3
         // table, c2 and c1 neutral or slower, so off there; profiles/r5/m, i)
         if (long_chain) h->yahead = 1;
-        // Under 1024 z tiles (c1: 128), packed: a wave per component in the z-pass, 3x the waves in flight
-        // (c1 z-pass 11.9 -> 9.0 us; c2's 2048 tiles and the reference grid's 2040 gain nothing;
-        // profiles/r2/ab_zsplit.jsonl)
-        if (h->coeff_mode == DF_COEFF_PACKED && (long long)h->nstrips * s.Ny < 1024) h->zsplit = 1;
+        // Up to 2048 z tiles with short chains (c1: 128, c2: 2048), packed: a wave per component in the z-pass,
+        // 3x the waves in flight (c1 z-pass 11.9 -> 9.0 us, profiles/r2/ab_zsplit.jsonl; c2 z-pass -2.5%, call
+        // -1%, 60-call windows in both orders, profiles/r5/n; the reference grid's 2040 long-chain tiles gain
+        // nothing)
+        const long long ztiles = (long long)h->nstrips * s.Ny;
+        if (h->coeff_mode == DF_COEFF_PACKED && (ztiles < 1024 || (!long_chain && ztiles <= 2048))) h->zsplit = 1;
     }
     // Planes of <= 1024 attempt blocks: K3 plans its own waves (one launch fewer: table mode the
     // reference's grid -5% per call, c1/c2 even; packed c2 -8..-10%, c1 -7%, profiles/r2/

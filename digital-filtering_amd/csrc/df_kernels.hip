@@ -2124,31 +2124,53 @@ __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
         double acc0 = 0.0, acc1 = 0.0;
         double2 P = ld_pair(xp);
         int m = 0;
-        // K noise pairs (2K taps) per step: the 2K coefficient loads and K pair loads issued first, then the
-        // products added in tap order (acc0: taps 2u with P[u].x, 2u+1 with P[u].y; acc1 one column on)
-        auto step = [&](auto KC) {
-            constexpr int K = decltype(KC)::value;
-            for (; m + K <= N; m += K) {
-                double2 Pn[K + 1];
-                Pn[0] = P;
+        if (ZU >= 4) {
+            for (; m + 4 <= N; m += 4) { // 8 taps: 8 coefficient loads + 4 noise pairs in flight
+                const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2), P3 = ld_pair(xp + m + 3), P4 = ld_pair(xp + m + 4);
+                double2 b[8];
 #pragma unroll
-                for (int u = 1; u <= K; ++u) Pn[u] = ld_pair(xp + m + u);
-                double2 b[2 * K];
-#pragma unroll
-                for (int u = 0; u < 2 * K; ++u) b[u] = coef(2 * m + u);
-#pragma unroll
-                for (int u = 0; u < K; ++u) {
-                    acc0 += b[2 * u].x * Pn[u].x;
-                    acc1 += b[2 * u].y * Pn[u].y;
-                    acc0 += b[2 * u + 1].x * Pn[u].y;
-                    acc1 += b[2 * u + 1].y * Pn[u + 1].x;
-                }
-                P = Pn[K];
+                for (int u = 0; u < 8; ++u) b[u] = coef(2 * m + u);
+                acc0 += b[0].x * P.x;
+                acc1 += b[0].y * P.y;
+                acc0 += b[1].x * P.y;
+                acc1 += b[1].y * P1.x;
+                acc0 += b[2].x * P1.x;
+                acc1 += b[2].y * P1.y;
+                acc0 += b[3].x * P1.y;
+                acc1 += b[3].y * P2.x;
+                acc0 += b[4].x * P2.x;
+                acc1 += b[4].y * P2.y;
+                acc0 += b[5].x * P2.y;
+                acc1 += b[5].y * P3.x;
+                acc0 += b[6].x * P3.x;
+                acc1 += b[6].y * P3.y;
+                acc0 += b[7].x * P3.y;
+                acc1 += b[7].y * P4.x;
+                P = P4;
             }
-        };
-        if constexpr (ZU >= 4) step(ic_t<4>{});
-        step(ic_t<2>{});
-        step(ic_t<1>{});
+        }
+        for (; m + 2 <= N; m += 2) {
+            const double2 P1 = ld_pair(xp + m + 1), P2 = ld_pair(xp + m + 2);
+            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1), b2 = coef(2 * m + 2), b3 = coef(2 * m + 3);
+            acc0 += b0.x * P.x;
+            acc1 += b0.y * P.y;
+            acc0 += b1.x * P.y;
+            acc1 += b1.y * P1.x;
+            acc0 += b2.x * P1.x;
+            acc1 += b2.y * P1.y;
+            acc0 += b3.x * P1.y;
+            acc1 += b3.y * P2.x;
+            P = P2;
+        }
+        for (; m < N; ++m) {
+            const double2 P1 = ld_pair(xp + m + 1);
+            const double2 b0 = coef(2 * m), b1 = coef(2 * m + 1);
+            acc0 += b0.x * P.x;
+            acc1 += b0.y * P.y;
+            acc0 += b1.x * P.y;
+            acc1 += b1.y * P1.x;
+            P = P1;
+        }
         const double2 bl = coef(2 * N);
         acc0 += bl.x * P.x;
         acc1 += bl.y * P.y;

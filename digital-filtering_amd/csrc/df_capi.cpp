@@ -1466,7 +1466,7 @@ int upload_tables(df_handle *h)
     // where it hangs past a row's first or last tap, and a zero tap leaves the sum bit for bit (+0 + (+-0) = +0
     // before the first tap, x + (+-0) = x after the last); the first kTabGuard entries are zeros for rows with
     // no tap in a chunk. Also the slack of the other sweeps' whole-window scalar loads.
-    constexpr int kTabGuard = 16;
+    constexpr int kTabGuard = 24; // >= the longest ypass_t64 chunk (yt_chunk)
     for (auto &kv : s.coeffs) {
         tabf_h.resize((tabf_h.size() + kTabGuard + 7) / 8 * 8, 0.0);
         tabf_off_h[kv.first] = (int)tabf_h.size();
@@ -2556,18 +2556,19 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {
         if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
-        if (value == 4 && h->yt_rows != 1) return fail(DF_EINVAL, "yt_pd 4 is built for yt_rows 1 only");
+        if (value == 4 && (h->yt_rows != 1 || h->yt_chunk != 16))
+            return fail(DF_EINVAL, "yt_pd 4 is built for yt_rows 1 x yt_chunk 16 only");
         h->yt_pd = value;
-    } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 2 x 8, 2 x 16
+    } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk): 1 x 16, 1 x 24, 2 x 8, 2 x 16
         const int R = k == "yt_rows" ? value : h->yt_rows, C = k == "yt_chunk" ? value : h->yt_chunk;
         const int Cu = k == "yt_rows" && !(R == 2 && C == 8) ? 16 : C; // a row count alone takes chunks of 16
-        if (!((R == 1 && Cu == 16) || (R == 2 && (Cu == 8 || Cu == 16))))
-            return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 2 x 8 or 2 x 16");
+        if (!((R == 1 && (Cu == 16 || Cu == 24)) || (R == 2 && (Cu == 8 || Cu == 16))))
+            return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 1 x 24, 2 x 8 or 2 x 16");
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
         h->yt_rows = R;
         h->yt_chunk = Cu;
-        if (R != 1) h->yt_pd = 2;
+        if (R != 1 || Cu != 16) h->yt_pd = 2;
         if (int rc = build_ylists(h)) return rc;
     }
     else if (k == "halo_ghost") { // the same on every rank of a plane (it decides whether a halo exchange runs)

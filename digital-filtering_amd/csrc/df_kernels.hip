@@ -1930,11 +1930,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
         if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
             const dim3 grid((unsigned)a.ylist_n);
             // R x C coefficients of a chunk held in SGPRs (24 doubles at most: more spill)
-            // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 2 x 16 26.6, 2 x 8 35-39, the
-            // round-4 ypass_tlds 40.4; 4 chunks in flight lose (VGPRs 38 -> 114) except on a lone block
+            // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 1 x 24 26.6 (the call beside the
+            // RNG -2%, profiles/r5/p), 2 x 16 26.6, 2 x 8 35-39, the round-4 ypass_tlds 40.4; 4 chunks in flight lose
+            // (VGPRs 38 -> 114) except on a lone block
             switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
             case 1162: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
             case 1164: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 4>), grid, dim3(256), 0, st, a); break;
+            case 1242: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 24, 2>), grid, dim3(256), 0, st, a); break;
             case 2082: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 8, 2>), grid, dim3(256), 0, st, a); break;
             case 2162: hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
             default: return hipErrorInvalidValue; // df_set_tuning admits the pairs above only

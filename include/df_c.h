@@ -221,8 +221,8 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
  *   sets such handles allocate at create), "ylds" (table y-pass with LDS-staged noise:
  *   2 = a block per (strip, 4 rows), 3 = a block per (64 columns, 4 waves of "yt_rows" rows) walking the
  *   tap window in "yt_chunk"-row chunks through a double-buffered LDS ring, "yt_pd" chunks of noise loads
- *   in flight, heaviest first; 0 = a wave per tile), "yt_rows" x "yt_chunk" (1 x 16 default, 2 x 8,
- *   2 x 16), "yt_pd" (2; 4 for yt_rows 1: deeper prefetch, more VGPRs), "zsplit" (packed z-pass, a wave
+ *   in flight, heaviest first; 0 = a wave per tile), "yt_rows" x "yt_chunk" (1 x 16 default, 1 x 24: on
+ *   the reference's grid the call -2% beside the RNG, the kernel alone +7%; 2 x 8, 2 x 16), "yt_pd" (2; 4 for yt_rows 1: deeper prefetch, more VGPRs), "zsplit" (packed z-pass, a wave
  *   per component: few-tile planes), "zstage" (table z-pass noise staged in LDS: 2 default, 0 the unstaged
  *   form large halos take), "nt_stores" (non-temporal output stores), "ywin_T" / "ywin_W" / "zwin_T" /
  *   "zwin_W" (sweep write windows: packed planes streaming >= 2 GB of coefficients).

@@ -1,7 +1,7 @@
 set -o pipefail
 # the round's closing evidence: full GPU suite, smoke, default bench, its rocprofv3 summary
 cd $GRAFT_REPO_ROOT
-O=gpurun_out/final; mkdir -p $O
+O=gpurun_out/${FINAL_TAG:-final}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?; tail -2 $O/tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
 tail -2 $O/smoke.log

@@ -586,7 +586,7 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
 int phase_ypass(df_handle *h, int comps_mask, int set = -1, hipStream_t st = nullptr);
 
 // The epoch just generated: its y-passes on ystream, ev_swept after them (df_handle::yahead)
-int sweep_ahead(df_handle *h, long long e, hipStream_t rs)
+int sweep_ahead(df_handle *h, long long e)
 {
     const bool on = h->yahead && h->overlap && h->ystream;
     h->ep_swept[e & 1] = on;
@@ -602,7 +602,6 @@ int sweep_ahead(df_handle *h, long long e, hipStream_t rs)
         h->yev[h->yev_used++].n = h->hb;
     }
     HIP_OR(hipEventRecord(h->ev_swept[e & 1], h->ystream), DF_EHIP);
-    (void)rs;
     return DF_OK;
 }
 
@@ -620,7 +619,7 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
     if (gen_pos(h, gi) == h->hb - 1) { // the epoch's noise is ready
         HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
         h->gen_launched++;
-        return sweep_ahead(h, gen_epoch(h, gi), rs);
+        return sweep_ahead(h, gen_epoch(h, gi));
     }
     h->gen_launched++;
     return DF_OK;
@@ -1100,21 +1099,17 @@ void balance_ycoop2(df_handle *h, int c)
                 nmax = std::max(nmax, Nst[(size_t)st * Ny + j]);
             }
             const int tile = st * nrb + rb;
-            if (h->ycoop_split4 > 0 && live == kStrip && nmax >= h->ycoop_split4) {
-                for (int part = 3; part <= 6; ++part) {
-                    wgt.push_back(taps * 32 + ovh);
-                    code.push_back(tile * 8 + part);
-                }
-            } else if (h->ycoop_split > 0 && live > 64 && nmax >= h->ycoop_split) {
-                for (int part = 1; part <= 2; ++part) {
-                    wgt.push_back(taps * (part == 1 ? 64 : live - 64) + ovh);
-                    code.push_back(tile * 8 + part);
-                }
-            } else {
-                wgt.push_back(taps * live + ovh);
-                code.push_back(tile * 8);
-            }
-            tot += taps * live + ovh;
+            auto item = [&](double w, int part) {
+                wgt.push_back(w);
+                code.push_back(tile * 8 + part);
+                tot += w;
+            };
+            if (h->ycoop_split4 > 0 && live == kStrip && nmax >= h->ycoop_split4)
+                for (int part = 3; part <= 6; ++part) item(taps * 32 + ovh, part);
+            else if (h->ycoop_split > 0 && live > 64 && nmax >= h->ycoop_split)
+                for (int part = 1; part <= 2; ++part) item(taps * (part == 1 ? 64 : live - 64) + ovh, part);
+            else
+                item(taps * live + ovh, 0);
         }
     }
     int *xr = h->c[c].ycoop2_xcd;

@@ -740,11 +740,9 @@ int prefetch_gen(df_handle *h)
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
     (void)gi;
-    // handles with three epochs of sets (y-pass ahead: consumed, swept, generating; single-GPU table planes:
-    // consumed and two generating) generate two epochs on: an ahead epoch's y-passes never wait for its own
-    // generation to start behind the release of the epoch before, and a table plane's VALU-bound generation
-    // gets a whole epoch of slack to fill the sweeps' gaps
-    const int depth = (h->hb > 1 || (h->yahead && h->ystream)) && epoch_slots(h) >= 3 ? 2 : 1;
+    // ahead handles hold three epochs of sets (consumed, swept, generating): generation two epochs on, so an
+    // epoch's y-passes never wait for its own generation to start behind the release of the epoch before
+    const int depth = h->yahead && h->ystream && epoch_slots(h) >= 3 ? 2 : 1;
     const long long need = h->gen_used + (fused_active(h) ? h->look : depth * h->hb);
     int rc;
     while (h->gen_launched < need)
@@ -1942,13 +1940,10 @@ int build(df_handle *h, const df_config_c *cfg)
     // the halo exchange (one c4/8 rank with a 40 us stand-in exchange: 0.244 / 0.238 -> 0.215 / 0.210 ms, ranks
     // 0 / 4; 0.196-0.198 either way without it; profiles/r5/d/strip.jsonl)
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->yahead = 1;
-    // ahead handles and single-GPU table planes hold three epochs of noise sets (prefetch_gen): the latter
-    // generate two epochs ahead (same-box A/B of two builds, 60-call windows: c3 table 0.334-0.338 ->
-    // 0.327 ms, c2 table -2%; profiles/r5/r)
+    // ahead handles hold three epochs of noise sets (consumed, swept ahead, generating)
     h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
-    if (h->yahead || (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb > 1))
-        h->nsets = 3 * h->hb;
+    if (h->yahead) h->nsets = 3 * h->hb;
     // z-strip handles in table mode, one process per GPU (split counting, the fused exchange): generations two
     // calls ahead. look is consulted only by fused_active() handles (one generation per hand-off), so in-process
     // groups and batched handles keep look 1 and the noise sets their batch needs (a batched handle

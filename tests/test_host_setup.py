@@ -351,3 +351,39 @@ def test_launch_plan_defaults(plane, mode, expect):
     assert got == expect
     with pytest.raises(dfamd.DFError, match="unknown tuning"):
         f.get_tuning("warp_size")
+
+
+def test_round5_tuning_keys_validate_on_host_only_handles():
+    # the keys added in round 5 (t64 shapes, row-pair halves/quarters, y-pass ahead, ghost columns) are checked
+    # and read back without a device: a host-only handle creates no stream and launches nothing
+    f = host(coeff_mode="table")  # the reference's grid, row-uniform N: ypass_t64 by default
+    assert (f.get_tuning("yt_rows"), f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (1, 16, 2)
+    f.set_tuning("yt_chunk", 24)
+    assert (f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (24, 2)
+    with pytest.raises(dfamd.DFError, match="yt_pd 4"):
+        f.set_tuning("yt_pd", 4)  # built for 1 x 16 only
+    f.set_tuning("yt_chunk", 16)
+    f.set_tuning("yt_pd", 4)
+    f.set_tuning("yt_rows", 2)  # 2 x 16; the prefetch depth drops to 2
+    assert (f.get_tuning("yt_rows"), f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (2, 16, 2)
+    with pytest.raises(dfamd.DFError, match="yt_rows x yt_chunk"):
+        f.set_tuning("yt_chunk", 24)  # 2 x 24 is not built
+    for key in ("ycoop_split", "ycoop_split4"):
+        with pytest.raises(dfamd.DFError, match=key):
+            f.set_tuning(key, -1)
+        f.set_tuning(key, 0)
+        assert f.get_tuning(key) == 0
+    f.set_tuning("ypass_ahead", 0)
+    assert f.get_tuning("ypass_ahead") == 0
+    f.set_tuning("ypass_ahead", 1)
+    assert f.get_tuning("ypass_ahead") == 1
+    with pytest.raises(dfamd.DFError, match="halo_ghost"):
+        f.set_tuning("halo_ghost", 1)  # a single plane has no neighbours to stand in for
+    f.set_tuning("halo_ghost", 0)
+    p = host(coeff_mode="packed", plane="synthetic", Ny=64, Nz=300, N_min=2, N_max=12, rank=0, world=2)
+    with pytest.raises(dfamd.DFError, match="halo_ghost"):
+        p.set_tuning("halo_ghost", 1)  # table mode only
+    t = host(coeff_mode="table", plane="synthetic", Ny=64, Nz=300, N_min=2, N_max=12, rank=0, world=2)
+    for v in (1, 0, 1):
+        t.set_tuning("halo_ghost", v)
+        assert t.get_tuning("halo_ghost") == v

@@ -73,3 +73,21 @@ def test_summary_takes_the_slowest_rank():
     assert mg["halo_ms_per_call"] == {"max": 0.05, "min": 0.03}
     assert mg["halo_bytes_per_call"] == 2 * 3145728 and mg["rng_collective_bytes_per_call"] == 0
     assert s["roofline"]["rank"] == 1 and s["roofline"]["frac_by_rank"] == [0.75, 0.71]
+
+
+def test_summary_adds_the_whole_call_hbm_figure_for_packed_lines():
+    # roofline.call: every rank's algorithmic call bytes over the slowest rank's wall per call (packed only)
+    class Ctx:
+        world = 2
+    wl = bench.plan_workload("c4", 2)
+    comm = {"rccl_ranks": 2, "rng_collective": 0, "halo_bytes_sent": 0, "rng_bytes_received": 0}
+    recs = [_rec(0, 0.020, 0.03, 0.9, 0.75, comm), _rec(1, 0.022, 0.05, 0.95, 0.71, comm)]
+    for r in recs:
+        r["call_bytes"] = 5.5e9
+    s = bench.summarize(Ctx, wl, bench.parse(["--steps", "10"]), recs)
+    call = s["roofline"]["call"]
+    assert call["bytes"] == 11e9 and call["ms"] == pytest.approx(2.2)
+    assert call["achieved"] == pytest.approx(11e9 / 2.2e-3 / 1e9, rel=1e-4)
+    assert call["frac"] == pytest.approx(call["achieved"] / bench.HBM_PEAK_GBPS, rel=1e-3)
+    t = bench.summarize(Ctx, wl, bench.parse(["--steps", "10", "--coeff-mode", "table"]), recs)
+    assert "call" not in t["roofline"]  # the byte model prices the packed stream only

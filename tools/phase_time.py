@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-phase device time of filter(dt) for one handle (timing experiments; not a test).
 
-    python3 tools/phase_time.py --config c3      (DFAMD_LIB=<another build of libdfamd.so> to time that one)
+    python3 tools/phase_time.py --config c3|native|...  (DFAMD_LIB=<another build of libdfamd.so> to time that one)
 
 Prints one JSON line: median over rounds of the hipEvent phase times (ms per call).
 """
@@ -28,9 +28,12 @@ def main():
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--tune", default="")
     a = ap.parse_args()
-    Ny, Nz, lo, hi = CFG[a.config]
-    f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=lo, N_max=hi, seed=1, device=0,
-                            coeff_mode=a.mode)
+    if a.config == "native":  # the reference's own 510 x 400 grid
+        f = dfamd.DigitalFilter(plane="native", seed=1, device=0, coeff_mode=a.mode)
+    else:
+        Ny, Nz, lo, hi = CFG[a.config]
+        f = dfamd.DigitalFilter(plane="synthetic", Ny=Ny, Nz=Nz, N_min=lo, N_max=hi, seed=1, device=0,
+                                coeff_mode=a.mode)
     for kv in filter(None, a.tune.split(",")):
         k, v = kv.split("=")
         f.set_tuning(k, int(v))

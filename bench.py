@@ -397,7 +397,7 @@ def dropin_timing(args):
         for mode in ("table", "packed"):
             progress(f"drop-in timing {plane} {mode}")
             try:
-                r = subprocess.run([exe, "time", "native" if plane == "native" else "synth", *dims, mode, "20"],
+                r = subprocess.run([exe, "time", "native" if plane == "native" else "synth", *dims, mode, "60"],
                                    capture_output=True, text=True, timeout=300, check=True)
                 rec = json.loads(r.stdout.strip().splitlines()[-1])
                 d = rec["dropin_ms"]
@@ -688,8 +688,10 @@ def summarize(ctx, wl, args, recs):
         cb = sum(r["call_bytes"] for r in recs)
         gbs = cb / (ms * 1e-3) / 1e9
         out["roofline"] = dict(out["roofline"], call={
-            "bytes": cb, "ms": round(ms, 4), "achieved": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBPS, 4),
-            "note": "every sweep's algorithmic bytes of one call / ms_per_step (all ranks)"})
+            "bytes": cb, "ms": round(ms, 4), "achieved": round(gbs, 1),
+            "frac": round(gbs / (HBM_PEAK_GBPS * ctx.world), 4),
+            "note": "every sweep's algorithmic bytes of one call / ms_per_step (all ranks) / the peak of all ranks"})
+    if ctx.world > 1:
         cm = recs[0]["comm"] or {}
         out["multi_gpu"] = {
             "rccl_ranks": cm.get("rccl_ranks"),

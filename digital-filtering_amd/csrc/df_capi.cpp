@@ -1076,7 +1076,7 @@ int read_config(df_handle *h, const df_config_c *cfg)
 // Work items: a tile, or (ycoop_split) one 64-column half of a wide-stencil tile. A block's chunks are its chain
 // of dependent round trips, and every resident block gets about the same share of HBM, so a 27-chunk tile of the
 // reference's grid ends the launch long after the 4-chunk ones; its halves fold two tap groups into each wave
-// (as the narrow last strip does), so each walks the chain in half the chunks, in parallel. Code = tile * 4 +
+// (as the narrow last strip does), so each walks the chain in half the chunks, in parallel. Code = tile * 8 +
 // part (0 whole, 1-2 the 64-column halves, 3-6 the 32-column quarters; ycoop_split4).
 void balance_ycoop2(df_handle *h, int c)
 {
@@ -2027,6 +2027,8 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         if (!hs[r]) return fail(DF_EINVAL, "null handle in group");
         if (hs[r]->rank != r || hs[r]->world != n || hs[r]->comm)
             return fail(DF_EINVAL, "group handles must be ranks 0..n-1 of one plane, created without comm_id");
+        // before any strip consumes a generation: a refused call leaves every stream state as it was
+        if (hs[r]->ghost != hs[0]->ghost) return fail(DF_EINVAL, "halo_ghost differs between the strips of a group");
     }
     int rc;
     for (int r = 0; r < n; ++r) {
@@ -2038,8 +2040,6 @@ int group_step(df_handle **hs, int n, bool corr_sra, double dt)
         if (!h->ghost && (rc = phase_halo_pack(h))) return rc;
     }
     const bool ghost = hs[0]->ghost != 0;
-    for (int r = 0; r < n; ++r)
-        if (hs[r]->ghost != hs[0]->ghost) return fail(DF_EINVAL, "halo_ghost differs between the strips of a group");
     if (!ghost)
         for (int r = 0; r < n; ++r) HIP_OR(hipStreamSynchronize(hs[r]->stream), DF_EHIP);
     for (int r = 0; r < n; ++r) {
@@ -2709,17 +2709,33 @@ int df_get_profile(df_handle *h, df_profile *out)
     return rc;
 }
 
-int df_sync(df_handle *h)
+static int sync_errors(df_handle *h)
 {
-    if (!valid_dev(h)) return DF_EINVAL;
-    int rc = sync_all(h);
-    if (rc) return rc;
-    if ((rc = check_rng_error(h))) return rc;
+    if (int rc = check_rng_error(h)) return rc;
     if (const int bad = ((volatile int *)h->err_host)[1]) {
         h->err_host[1] = 0;
         return fail(DF_EINVAL, "df_gather_field: " + std::to_string(bad) + " out-of-range indices were skipped");
     }
     return DF_OK;
+}
+
+int df_sync(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    int rc = sync_all(h);
+    return rc ? rc : sync_errors(h);
+}
+
+// Every result a caller can see (fields, statistics, gathers, the stage API) is written on the handle's stream;
+// the RNG stream and ystream carry later calls' noise and y-passes (df_sync waited for those
+// too, on every step of a synchronous caller). The noise this call consumed was ready before its sweeps ran
+// (the stream waited for it), so its error flag is final here.
+int df_wait(df_handle *h)
+{
+    if (!valid_dev(h)) return DF_EINVAL;
+    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    return sync_errors(h);
 }
 
 int df_gather_field(df_handle *h, int which, long long n, const long long *plane_cell, double *dst,

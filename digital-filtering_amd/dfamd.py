@@ -115,6 +115,7 @@ def lib():
                                       C.c_double]),
         "df_get_profile": (C.c_int, [H, C.POINTER(Profile)]),
         "df_sync": (C.c_int, [H]),
+        "df_wait": (C.c_int, [H]),
         "df_stream": (C.c_void_p, [H]),
         "df_algorithmic_bytes": (C.c_double, [H, C.c_int]),
         "df_comm_unique_id": (C.c_int, [C.c_void_p, C.c_size_t]),
@@ -251,6 +252,10 @@ class DigitalFilter:
 
     def sync(self):
         _check(lib().df_sync(self._h))
+
+    def wait(self):
+        """This handle's results so far (df_wait), not the later calls' noise already queued."""
+        _check(lib().df_wait(self._h))
 
     # --- stage API (df.hpp:96-101)
     def generate_white_noise(self):

@@ -4,15 +4,19 @@
 //
 //   cpp-test                      native grid, like the reference (get_rms: 500 x filter(1e-5))
 //   cpp-test filter N dt          N x filter(dt), prints sum(u'^2)
-//   cpp-test synth Ny Nz Nmin Nmax seed steps [csv]   synthetic plane, writes u'/v'/w'/T'/rho' CSV
+//   cpp-test synth Ny Nz Nmin Nmax seed steps [csv [ordered]]   synthetic plane, writes u'/v'/w'/T'/rho' CSV;
+//                                 ordered: host_mirror 0 + stream_ordered (no host wait per call), one
+//                                 wait() and mirror refresh before the CSV
 //   cpp-test rms seed             native grid, seeded, get_rms() -> ../files/cpp_vel_fluc_rms.csv
 //   cpp-test writers seed dt steps out   native grid, steps x filter(dt), then write_tecplot(out) and
 //                                 plot_RST_lerp() -> ../files/myRST.csv, ../files/duanRST.csv
 //   cpp-test twin Ny Nz Nmin Nmax seed steps csvA csvB   two objects on the process's one stream
 //                                 (df.cpp:334-335): A then B constructed, filter calls alternating
 //   cpp-test time native|synth Ny Nz Nmin Nmax packed|table calls   one JSON line: wall ms per call
-//                                 of the C-ABI call (df_filter + df_sync) and of DIGITAL_FILTER::filter()
-//                                 with host_mirror 0, 1, 2 on the same object (bench.py `dropin`)
+//                                 of the C-ABI call (df_filter + df_wait: this call's fields; and + df_sync:
+//                                 everything queued, later calls' noise included) and of
+//                                 DIGITAL_FILTER::filter() with host_mirror 0, 1, 2 on the same object, and
+//                                 the y-pass-ahead setting flipped (bench.py `dropin`)
 #include "df.hpp"
 
 #include <cstdlib>
@@ -48,17 +52,32 @@ static int time_dropin(char **argv)
     };
     const double capi_async = wall([&] { ok(df_filter(h, 1e-8)); }) ; // queue only; the sync below drains
     ok(df_sync(h));
-    const double capi = wall([&] { ok(df_filter(h, 1e-8)); ok(df_sync(h)); });
+    const double capi_sync = wall([&] { ok(df_filter(h, 1e-8)); ok(df_sync(h)); });
+    const double capi = wall([&] { ok(df_filter(h, 1e-8)); ok(df_wait(h)); });
+    // the same per-call wait with the y-pass-ahead setting flipped (its default is decided on this figure)
+    int ahead = 0;
+    ok(df_get_tuning(h, "ypass_ahead", &ahead));
+    ok(df_set_tuning(h, "ypass_ahead", !ahead));
+    const double capi_flip = wall([&] { ok(df_filter(h, 1e-8)); ok(df_wait(h)); });
+    ok(df_set_tuning(h, "ypass_ahead", ahead));
+    ok(df_sync(h));
     double dropin[3];
     for (int m = 0; m < 3; ++m) {
         df.set_host_mirror(m);
         dropin[m] = wall([&] { df.filter(1e-8); });
     }
+    df.set_host_mirror(0);
+    df.set_stream_ordered(true); // no host wait: the caller orders its work on df.stream()
+    const double ordered = wall([&] { df.filter(1e-8); });
+    df.sync();
+    df.set_stream_ordered(false);
     std::cout << std::setprecision(6) << "{\"plane\": \"" << argv[2] << "\", \"Ny\": " << ny << ", \"Nz\": " << nz
               << ", \"coeff_mode\": \"" << argv[7] << "\", \"calls\": " << calls
-              << ", \"capi_ms\": " << capi << ", \"capi_async_ms\": " << capi_async
+              << ", \"capi_ms\": " << capi << ", \"capi_sync_all_ms\": " << capi_sync << ", \"capi_async_ms\": " << capi_async
+              << ", \"ypass_ahead\": " << ahead << ", \"capi_ms_ypass_ahead_flipped\": " << capi_flip
               << ", \"dropin_ms\": {\"mirror0\": " << dropin[0] << ", \"mirror1\": " << dropin[1]
-              << ", \"mirror2\": " << dropin[2] << "}, \"mirror_bytes\": {\"mirror1\": " << 5 * 8 * cells
+              << ", \"mirror2\": " << dropin[2] << ", \"mirror0_stream_ordered\": " << ordered
+              << "}, \"mirror_bytes\": {\"mirror1\": " << 5 * 8 * cells
               << ", \"mirror2\": " << 11 * 8 * cells << "}}" << std::endl;
     return 0;
 }
@@ -77,9 +96,18 @@ int main(int argc, char **argv)
         config.N_max = std::atoi(argv[5]);
         config.seed = std::strtoull(argv[6], nullptr, 10);
         config.seed_from_random_device = false;
+        const bool ordered = argc > 9 && std::string(argv[9]) == "ordered";
+        if (ordered) {
+            config.host_mirror = 0;
+            config.stream_ordered = true;
+        }
         DIGITAL_FILTER df(config);
         const int steps = std::atoi(argv[7]);
         for (int s = 0; s < steps; ++s) df.filter(1e-8);
+        if (ordered) {
+            df.wait();
+            df.sync_host();
+        }
         df.write_csv(argc > 8 ? argv[8] : "cpp_vel_fluc.csv");
         return 0;
     }

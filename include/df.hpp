@@ -128,6 +128,10 @@ struct DFConfig { // df.hpp:38-49; defaults = values hard-coded in df.cpp:7-16
     // and filt are refreshed on request (sync_host(), checkpoint()). 2: all of them after every call.
     // 0: never (a GPU-resident solver reads device_field()).
     int host_mirror = 1;
+    // With host_mirror 0: filter() returns as soon as the call is enqueued, no host wait at all; the caller
+    // orders its own work on stream() (df_stream: launch there, or hipStreamWaitEvent on an event recorded
+    // there) - the GPU-resident coupling of us3d_user.f90:80-120. "Filtering took" then times the enqueue.
+    bool stream_ordered = false;
     bool pin_mirrors = true;     // page-lock the mirror vectors (hipHostRegister via df_host_pin)
     int mirror_coefficients = -1; // by/bz host copies: 1 always, 0 never, -1 when <= 1 GiB
     bool verbose = true;         // print "Filtering took X seconds." (df.cpp:464)
@@ -421,7 +425,8 @@ class DIGITAL_FILTER {
         stream_in();
         auto start = NOW;
         check(df_filter(h_, dt));
-        check(df_sync(h_));
+        // the fields of this call, not the noise and y-passes already queued for later calls (df_wait)
+        if (!(cfg_.stream_ordered && cfg_.host_mirror == 0)) check(df_wait(h_));
         auto end = NOW;
         stream_out();
         if (cfg_.verbose) {
@@ -464,7 +469,7 @@ class DIGITAL_FILTER {
             check(df_rms_add(h_));
             rms_counter++;
         }
-        check(df_sync(h_));
+        check(df_wait(h_));
         stream_out();
         refresh();
         plot_rms();
@@ -578,6 +583,12 @@ class DIGITAL_FILTER {
 
     // ====== MI355X extensions
     df_handle *handle() { return h_; }
+    // The HIP stream (hipStream_t) every result is written on (DFConfig::stream_ordered), and the two waits:
+    // wait() = this object's results so far (df_wait), sync() = every queued call's work (df_sync).
+    void *stream() { return df_stream(h_); }
+    void wait() { check(df_wait(h_)); }
+    void sync() { check(df_sync(h_)); }
+    void set_stream_ordered(bool on) { cfg_.stream_ordered = on; }
     // Refresh every host mirror now (filt_old and filt included), whatever host_mirror says.
     void sync_host() { refresh_mirrors(true); }
     void set_host_mirror(int level) { cfg_.host_mirror = level; }

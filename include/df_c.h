@@ -253,7 +253,16 @@ int df_get_tuning(df_handle *h, const char *key, int *value);
  * queue packets between a call's kernels and cost up to 10% of a short call. */
 int df_set_profiling(df_handle *h, int on);
 int df_get_profile(df_handle *h, df_profile *out);
+/* Wait for ALL queued work of the handle: its results AND the noise generation / y-passes already enqueued
+ * for later calls (state loads, timing brackets, teardown). */
 int df_sync(df_handle *h);
+/* Wait for the results of the work enqueued so far - fields, T'/rho', statistics, gathers, the stage API -
+ * and nothing else: later calls' noise and y-passes keep running (df.cpp:449-468's filter() returns when
+ * its fields are done). The per-step wait of a synchronous caller (DIGITAL_FILTER::filter). Reports the
+ * same errors as df_sync. */
+int df_wait(df_handle *h);
+/* The HIP stream (hipStream_t) every result is written on: a GPU-resident caller orders its own work after
+ * df_filter with hipStreamWaitEvent / launches on this stream, no host wait at all. */
 void *df_stream(df_handle *h);
 /* Bytes of HBM the packed/table hot path must move per df_filter (SURVEY 8d model). */
 double df_algorithmic_bytes(df_handle *h, int kernel /* -1 whole call, 0 ypass, 1 zpass */);

@@ -153,6 +153,10 @@ module df_c_binding
             import :: c_ptr, c_int
             type(c_ptr), value :: h
         end function
+        integer(c_int) function df_wait(h) bind(C, name="df_wait")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+        end function
         type(c_ptr) function df_stream(h) bind(C, name="df_stream")
             import :: c_ptr
             type(c_ptr), value :: h

@@ -88,6 +88,21 @@ def test_summary_adds_the_whole_call_hbm_figure_for_packed_lines():
     call = s["roofline"]["call"]
     assert call["bytes"] == 11e9 and call["ms"] == pytest.approx(2.2)
     assert call["achieved"] == pytest.approx(11e9 / 2.2e-3 / 1e9, rel=1e-4)
-    assert call["frac"] == pytest.approx(call["achieved"] / bench.HBM_PEAK_GBPS, rel=1e-3)
+    # both ranks' bytes over both ranks' peak (one GPU's peak overstated it N times)
+    assert call["frac"] == pytest.approx(call["achieved"] / (2 * bench.HBM_PEAK_GBPS), rel=1e-3)
     t = bench.summarize(Ctx, wl, bench.parse(["--steps", "10", "--coeff-mode", "table"]), recs)
     assert "call" not in t["roofline"]  # the byte model prices the packed stream only
+    # table-mode multi-GPU lines keep their multi_gpu block (halo, RNG collective, per-rank times)
+    assert t["multi_gpu"]["rccl_ranks"] == 2 and len(t["multi_gpu"]["per_rank"]) == 2
+
+
+def test_single_gpu_summary_has_no_multi_gpu_block():
+    class Ctx:
+        world = 1
+    wl = bench.plan_workload("c3", 1)
+    rec = _rec(0, 0.020, 0.0, 1.7, 0.78, None)
+    rec["call_bytes"] = 21.26e9
+    s = bench.summarize(Ctx, wl, bench.parse(["--steps", "10"]), [rec])
+    assert "multi_gpu" not in s
+    assert s["roofline"]["call"]["frac"] == pytest.approx(s["roofline"]["call"]["achieved"] / bench.HBM_PEAK_GBPS,
+                                                          rel=1e-3)

@@ -60,10 +60,12 @@ def test_cpp_driver_get_rms_csv(tmp_path):
         assert np.allclose(va, vb, rtol=2e-6, atol=0), (a, b)
 
 
-def test_cpp_driver_filter_csv_matches_oracle(tmp_path):
+@pytest.mark.parametrize("ordered", [False, True])
+def test_cpp_driver_filter_csv_matches_oracle(tmp_path, ordered):
+    # ordered: DFConfig::stream_ordered with host_mirror 0 - filter() never waits on the host
     csv = tmp_path / "g.csv"
-    out = subprocess.run([EXE, "synth", "64", "96", "2", "10", "17", "3", str(csv)], capture_output=True,
-                         text=True, timeout=120)
+    out = subprocess.run([EXE, "synth", "64", "96", "2", "10", "17", "3", str(csv)] + (["ordered"] if ordered else []),
+                         capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert out.stdout.count("Filtering took") == 3
     o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=64, Nz=96, N_min=2, N_max=10, seed=17)
@@ -104,6 +106,36 @@ def test_cpp_two_objects_share_the_process_stream(tmp_path):
     A = np.loadtxt(a_csv, delimiter=",", skiprows=1)
     B = np.loadtxt(b_csv, delimiter=",", skiprows=1)
     assert float(np.abs(A[:, 2:] - B[:, 2:]).max()) > 0
+
+
+def _hip_memcpy_d2h(dst, src_ptr, nbytes):
+    """hipMemcpy on the null stream: the handle's streams are non-blocking, so this copy waits for none of
+    them - whatever the field holds once the host returns from df_wait is what it reads."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipMemcpy(ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src_ptr), ctypes.c_size_t(nbytes), 2)
+    assert rc == 0, rc
+
+
+@pytest.mark.parametrize("plane", [dict(plane="native"), dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32)])
+@pytest.mark.parametrize("mode", ["table", "packed"])
+def test_df_wait_covers_the_call_fields(plane, mode):
+    # df_wait waits for the handle's stream only - not the RNG stream / ystream carrying later calls' noise and
+    # y-passes - and that is every write a filter() result depends on: after 6 asynchronous calls and one
+    # df_wait, a copy that orders after none of the handle's streams reads the oracle's fields
+    f = dfamd.DigitalFilter(seed=31, device=0, coeff_mode=mode, **plane)
+    o = O.Filter(plane=O.PLANE_NATIVE, seed=31) if plane["plane"] == "native" else O.Filter(
+        plane=O.PLANE_SYNTHETIC, Ny=plane["Ny"], Nz=plane["Nz"], N_min=plane["N_min"], N_max=plane["N_max"], seed=31)
+    for _ in range(6):
+        f.filter(1e-8)
+        o.filter(1e-8)
+    f.wait()
+    for i, k in enumerate(FIELDS):
+        ref = o.field(k)
+        got = np.empty_like(ref)
+        _hip_memcpy_d2h(got, f.device_ptr(k), got.nbytes)
+        assert np.array_equal(got, ref), k
+    assert f.rng_state() == o.rng.state
 
 
 def test_variance_invariant_over_time():

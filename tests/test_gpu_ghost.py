@@ -62,6 +62,23 @@ def test_ghost_toggled_mid_run_and_noise_arrays():
         assert np.array_equal(got, ry), c
 
 
+def test_ghost_disagreement_is_refused_before_any_strip_draws():
+    # a group call whose strips disagree on halo_ghost fails before any strip consumes a generation,
+    # so once they agree the run continues in step with the reference
+    spec = dict(plane="synthetic", Ny=64, Nz=600, N_min=4, N_max=24, seed=29, device=0, coeff_mode="table")
+    o = O.Filter(plane=O.PLANE_SYNTHETIC, Ny=64, Nz=600, N_min=4, N_max=24, seed=29)
+    hs = dfamd.create_group(3, **spec)
+    hs[1].set_tuning("halo_ghost", 1)
+    with pytest.raises(dfamd.DFError, match="halo_ghost differs"):
+        dfamd.filter_group(hs, 1e-8)
+    hs[0].set_tuning("halo_ghost", 1)
+    hs[2].set_tuning("halo_ghost", 1)
+    for i in range(2):
+        o.filter(1e-8)
+        dfamd.filter_group(hs, 1e-8)
+        check(hs, o, f"call {i} after the refused call")
+
+
 def test_ghost_needs_table_mode_and_row_uniform_planes():
     packed = dfamd.create_group(2, plane="synthetic", Ny=40, Nz=300, N_min=4, N_max=8, seed=1, device=0,
                                 coeff_mode="packed")

@@ -257,6 +257,10 @@ struct df_handle {
     double prof_y_span = 0, prof_y_main = 0; // ms: ahead spans; y-passes on the stream
     long long prof_y_n = 0, prof_y_calls = 0; // y-passes in the spans; profiled calls whose y-pass ran ahead
     std::vector<void *> allocs;
+    // Schedule trace (a handle created with device = DF_DEVICE_TRACE): the noise pipeline's host logic runs with
+    // every HIP call it would make replaced by a record (trace_*), six int64 per record, read by df_trace
+    bool tracing = false;
+    std::vector<long long> tr;
 };
 
 namespace {
@@ -460,6 +464,56 @@ int check_rng_error(df_handle *h)
 
 bool prof_on(df_handle *h) { return h->profiling && h->prof_call && h->ev_used < h->ev.size(); }
 
+// ---------------------------------------------------------------- schedule trace
+// A DF_DEVICE_TRACE handle has no GPU: its streams and events are stand-in handles (kTrStream + i, kTrEvent + id) and
+// each operation the pipeline would enqueue becomes one record {op, stream, a, b, c, d} (tests/test_schedule.py
+// rebuilds the happens-before order from them and checks every noise set, stream state slot and event wait).
+enum TraceOp {
+    TR_RECORD = 1, // stream, event, tag: the event recorded (tag: the generation whose work it follows)
+    TR_WAIT,       // stream, event, tag: the stream waits for the event's latest record (tag: the intended one)
+    TR_K1,         // stream, gen, state slot read: attempt counts into the RNG scratch
+    TR_K3,         // stream, gen, set, slot in, slot out: scratch + state in -> the set's r_ys and r_zs pads, state out
+    TR_SHARE,      // stream, gen: the other ranks' share records into the scratch (solo-strip stand-in)
+    TR_YPASS,      // stream, gen, set: r_ys of the set -> its r_zs interior
+    TR_PACK,       // stream, gen, set: halo columns read from the set's r_zs interior
+    TR_ZPASS,      // stream, gen, set: the set's r_zs -> the fields
+    TR_SYNC,       // every stream drained by the host
+    TR_STATE_R,    // -, slot, gen: the host reads the stream state before generation gen (df_rng_state)
+    TR_STATE_W     // -, slot, gen: the host writes it (df_set_rng_state, the seed at create)
+};
+enum TraceEvent { TE_RNG = 0, TE_SWEPT = 2, TE_RELEASE = 4, TE_COUNTED = 4 + kMaxNoiseSets, TE_XCHG, TE_HALO, TE_N };
+constexpr uintptr_t kTrStream = 0x10, kTrEvent = 0x100;
+long long tr_stream(hipStream_t st) { return (long long)((uintptr_t)st - kTrStream); }
+long long tr_event(hipEvent_t ev) { return (long long)((uintptr_t)ev - kTrEvent); }
+void trace(df_handle *h, long long op, long long st = -1, long long a = 0, long long b = 0, long long c = 0,
+           long long d = 0)
+{
+    h->tr.insert(h->tr.end(), {op, st, a, b, c, d});
+}
+// hipEventRecord / hipStreamWaitEvent of the pipeline; tag = the generation the record follows / the wait means
+int q_record(df_handle *h, hipEvent_t ev, hipStream_t st, long long tag)
+{
+    if (h->tracing) {
+        trace(h, TR_RECORD, tr_stream(st), tr_event(ev), tag);
+        return DF_OK;
+    }
+    HIP_OR(hipEventRecord(ev, st), DF_EHIP);
+    return DF_OK;
+}
+int q_wait(df_handle *h, hipStream_t st, hipEvent_t ev, long long tag)
+{
+    if (h->tracing) {
+        trace(h, TR_WAIT, tr_stream(st), tr_event(ev), tag);
+        return DF_OK;
+    }
+    HIP_OR(hipStreamWaitEvent(st, ev, 0), DF_EHIP);
+    return DF_OK;
+}
+#define Q_OR(expr)                                                                                          \
+    do {                                                                                                    \
+        if (int rc_ = (expr)) return rc_;                                                                   \
+    } while (0)
+
 void ev_record(df_handle *h, int phase, hipStream_t st = nullptr)
 {
     if (!prof_on(h)) return;
@@ -468,6 +522,10 @@ void ev_record(df_handle *h, int phase, hipStream_t st = nullptr)
 
 int sync_all(df_handle *h)
 {
+    if (h->tracing) {
+        trace(h, TR_SYNC);
+        return DF_OK;
+    }
     HIP_OR(hipStreamSynchronize(h->rng_stream), DF_EHIP);
     if (h->ystream) HIP_OR(hipStreamSynchronize(h->ystream), DF_EHIP);
     HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
@@ -548,7 +606,8 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
     rs = h->overlap ? h->rng_stream : h->stream;
     // the epoch's sets were last read by epoch e - K (K = epoch_slots), released when epoch e - K + 1 began
     const int K = epoch_slots(h);
-    if (gen_pos(h, gi) == 0 && e >= K) HIP_OR(hipStreamWaitEvent(rs, h->ev_release[e % K], 0), DF_EHIP);
+    // (its last generation: gi - nsets + hb - 1)
+    if (gen_pos(h, gi) == 0 && e >= K) Q_OR(q_wait(h, rs, h->ev_release[e % K], gi - h->nsets + h->hb - 1));
     g = h->geom;
     g.recount = h->split_count ? 1 : 0;
     // small single-plane calls: the compacted K3 computes its waves' ranks and plan itself
@@ -571,6 +630,10 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
         ev_record(h, 4);
         h->ev[h->ev_used].rng = true;
     }
+    if (h->tracing) {
+        trace(h, TR_K1, tr_stream(rs), gi, gen_set(h, gi));
+        return DF_OK;
+    }
     const RngStateDev *in = h->rstate + gen_set(h, gi);
     if (!h->split_count)
         HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs),
@@ -583,7 +646,10 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
     return DF_OK;
 }
 
-int phase_ypass(df_handle *h, int comps_mask, int set = -1, hipStream_t st = nullptr);
+int phase_ypass(df_handle *h, int comps_mask, int set = -1, hipStream_t st = nullptr, long long gen = -1);
+
+// The last generation of epoch e (gen_epoch's inverse)
+long long epoch_last(const df_handle *h, long long e) { return h->hb == 1 ? e : h->gen_base + e * h->hb + h->hb - 1; }
 
 // The epoch just generated: its y-passes on ystream, ev_swept after them (df_handle::yahead)
 int sweep_ahead(df_handle *h, long long e)
@@ -591,18 +657,17 @@ int sweep_ahead(df_handle *h, long long e)
     const bool on = h->yahead && h->overlap && h->ystream;
     h->ep_swept[e & 1] = on;
     if (!on) return DF_OK;
-    HIP_OR(hipStreamWaitEvent(h->ystream, h->ev_rng[e & 1], 0), DF_EHIP);
+    Q_OR(q_wait(h, h->ystream, h->ev_rng[e & 1], epoch_last(h, e)));
     const bool timed = h->profiling && (h->yev_seq++ % h->profile_every) == 0 && h->yev_used < h->yev.size();
     if (timed) HIP_OR(hipEventRecord(h->yev[h->yev_used].e[0], h->ystream), DF_EHIP);
     const long long g0 = h->hb == 1 ? e : h->gen_base + e * h->hb;
     for (long long g = g0; g < g0 + h->hb; ++g)
-        if (int rc = phase_ypass(h, 7, gen_set(h, g), h->ystream)) return rc;
+        if (int rc = phase_ypass(h, 7, gen_set(h, g), h->ystream, g)) return rc;
     if (timed) {
         HIP_OR(hipEventRecord(h->yev[h->yev_used].e[1], h->ystream), DF_EHIP);
         h->yev[h->yev_used++].n = h->hb;
     }
-    HIP_OR(hipEventRecord(h->ev_swept[e & 1], h->ystream), DF_EHIP);
-    return DF_OK;
+    return q_record(h, h->ev_swept[e & 1], h->ystream, epoch_last(h, e));
 }
 
 int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
@@ -611,13 +676,16 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
     // split counting exchanges counts only: K3 recomputes the accept flags of the waves it runs
     // (g.recount), a sixth or less of all waves on an interior rank of 8
-    HIP_OR(launch_rng_finish(g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->counts,
-                             h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks, h->err_dev,
-                             h->rng_blocks, nb_scan, rs),
-           DF_EHIP);
+    if (h->tracing)
+        trace(h, TR_K3, tr_stream(rs), gi, gen_set(h, gi), gen_set(h, gi), gen_set(h, gi + 1));
+    else
+        HIP_OR(launch_rng_finish(g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->counts,
+                                 h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks, h->err_dev,
+                                 h->rng_blocks, nb_scan, rs),
+               DF_EHIP);
     if (prof_on(h)) ev_record(h, 5, rs);
     if (gen_pos(h, gi) == h->hb - 1) { // the epoch's noise is ready
-        HIP_OR(hipEventRecord(h->ev_rng[gen_epoch(h, gi) & 1], rs), DF_EHIP);
+        Q_OR(q_record(h, h->ev_rng[gen_epoch(h, gi) & 1], rs, gi));
         h->gen_launched++;
         return sweep_ahead(h, gen_epoch(h, gi));
     }
@@ -680,7 +748,9 @@ int launch_gen(df_handle *h)
         int *wmine = h->wave_counts + (size_t)h->rank * nwc;
         const size_t ngc = (size_t)g.xstride;
         uint8_t *gmine = g.xbuf + (size_t)h->rank * ngc;
-        if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
+        if (h->tracing && !h->rng_comm) {
+            trace(h, TR_SHARE, tr_stream(rs), h->gen_launched);
+        } else if (h->rng_comm) { // the RNG's one exchange: accept counts per block and per wave
             // Never concurrent with the halo send/recv of the other communicator: every rank issues
             // the all-gather only after its own halo group of the call just enqueued has completed,
             // so the two communicators' kernels run in the same order on every rank.
@@ -717,12 +787,12 @@ int consume_gen(df_handle *h)
     const bool first = gen_pos(h, gi) == 0;
     int rc;
     if (first && gi > (h->hb == 1 ? 0 : h->gen_base))
-        HIP_OR(hipEventRecord(h->ev_release[(e - 1) % epoch_slots(h)], h->stream), DF_EHIP); // the previous epoch's sets free
+        Q_OR(q_record(h, h->ev_release[(e - 1) % epoch_slots(h)], h->stream, gi - 1)); // the previous epoch's sets free
     const long long need = h->hb == 1 ? gi + 1 : h->gen_base + (e + 1) * h->hb; // this epoch, launched
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
     h->cur_swept = h->ep_swept[e & 1];
-    if (first) HIP_OR(hipStreamWaitEvent(h->stream, (h->cur_swept ? h->ev_swept : h->ev_rng)[e & 1], 0), DF_EHIP);
+    if (first) Q_OR(q_wait(h, h->stream, (h->cur_swept ? h->ev_swept : h->ev_rng)[e & 1], need - 1));
     h->cur = gen_set(h, gi);
     h->gen_used++;
     return DF_OK;
@@ -734,20 +804,29 @@ int consume_gen(df_handle *h)
 // under the last step of epoch e, just before epoch e + 1 waits for it.
 int fused_gen_end(df_handle *h);
 bool fused_active(const df_handle *h);
+int prefetch_epochs(const df_handle *h);
 int prefetch_gen(df_handle *h)
 {
     if (int rc = fused_gen_end(h)) return rc;
     if (!h->overlap || h->gen_used == 0) return DF_OK;
     const long long gi = h->gen_used - 1; // the generation this step consumed
     (void)gi;
-    // ahead handles hold three epochs of sets (consumed, swept, generating): generation two epochs on, so an
-    // epoch's y-passes never wait for its own generation to start behind the release of the epoch before
-    const int depth = h->yahead && h->ystream && epoch_slots(h) >= 3 ? 2 : 1;
-    const long long need = h->gen_used + (fused_active(h) ? h->look : depth * h->hb);
+    const long long need = h->gen_used + (fused_active(h) ? h->look : prefetch_epochs(h) * h->hb);
     int rc;
     while (h->gen_launched < need)
         if ((rc = launch_gen(h))) return rc;
     return DF_OK;
+}
+
+// Epochs generated ahead of the one being consumed. Two where three epochs of sets are held (epoch_slots >= 3) and
+// the handle batches or runs the y-pass ahead: ahead handles (consumed, swept, generating) so an epoch's y-passes
+// never wait for its own generation to start behind the release of the epoch before; batched single-GPU table
+// planes so their VALU-bound generation has a whole epoch of slack to fill the sweeps' gaps. Never more than
+// epoch_slots - 1: generation of epoch e waits for the release of epoch e - epoch_slots, recorded when epoch
+// e - epoch_slots + 1 begins (tests/test_schedule.py checks every schedule on the host).
+int prefetch_epochs(const df_handle *h)
+{
+    return (h->hb > 1 || (h->yahead && (h->ystream || h->device < 0))) && epoch_slots(h) >= 3 ? 2 : 1;
 }
 
 // The fused exchange applies to split-counting z-strip handles of one process per GPU (RCCL, or the solo-strip
@@ -767,7 +846,7 @@ int fused_gen_begin(df_handle *h)
     int rc = gen_begin(h, h->pend_g, rs);
     if (rc) return rc;
     if (h->pend_g.gen_dense != 2) return DF_OK; // cannot happen with fused_active; the plain path then runs
-    HIP_OR(hipEventRecord(h->ev_counted, rs), DF_EHIP);
+    Q_OR(q_record(h, h->ev_counted, rs, h->gen_launched));
     h->gen_pending = true;
     if (h->ghost) { // no halo group to ride in: the records' all-gather follows the counts on the RNG stream, so
                     // the sweep stream never waits on a collective (the sweeps of calls k, k + 1 run beside it)
@@ -776,8 +855,8 @@ int fused_gen_begin(df_handle *h)
             NCCL_OR(ncclAllGather(h->pend_g.xbuf + (size_t)h->rank * ngc, h->pend_g.xbuf, ngc, ncclUint8, h->rng_comm, rs));
             HIP_OR(hipEventRecord(h->ev_halo, rs), DF_EHIP);
         } else { // solo strip: the exchange's stand-in (and its held time) on the RNG stream
-            if (h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, rs), DF_EHIP);
-            HIP_OR(hipEventRecord(h->ev_xchg, rs), DF_EHIP);
+            if (h->solo_xchg_us > 0 && !h->tracing) HIP_OR(launch_hold(h->solo_xchg_us, rs), DF_EHIP);
+            Q_OR(q_record(h, h->ev_xchg, rs, h->gen_launched));
         }
     }
     return DF_OK;
@@ -792,14 +871,19 @@ int fused_gen_end(df_handle *h)
     if (h->comm) {
         HIP_OR(hipStreamWaitEvent(rs, h->ev_halo, 0), DF_EHIP);
     } else { // solo strip: the same dependency on this call's halo position, the exchange by a stand-in copy
-        HIP_OR(hipStreamWaitEvent(rs, h->ev_xchg, 0), DF_EHIP);
-        HIP_OR(launch_replicate_share(h->pend_g.xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
+        Q_OR(q_wait(h, rs, h->ev_xchg, h->gen_launched));
+        if (h->tracing) trace(h, TR_SHARE, tr_stream(rs), h->gen_launched);
+        else HIP_OR(launch_replicate_share(h->pend_g.xbuf, (size_t)h->pend_g.xstride, h->world, h->rank, rs), DF_EHIP);
     }
     return gen_end(h, h->pend_g, rs);
 }
 
-int phase_ypass(df_handle *h, int comps_mask, int set, hipStream_t st)
+int phase_ypass(df_handle *h, int comps_mask, int set, hipStream_t st, long long gen)
 {
+    if (h->tracing) {
+        trace(h, TR_YPASS, tr_stream(st ? st : h->stream), gen >= 0 ? gen : h->gen_used - 1, set >= 0 ? set : h->cur);
+        return DF_OK;
+    }
     SweepArgs a = sweep_args(h);
     a.comps_mask = comps_mask;
     if (set >= 0)
@@ -828,6 +912,10 @@ int phase_ypass(df_handle *h, int comps_mask, int set, hipStream_t st)
 int phase_halo_pack(df_handle *h)
 {
     if (h->world == 1) return DF_OK;
+    if (h->tracing) {
+        trace(h, TR_PACK, tr_stream(h->stream), h->gen_used - 1, h->cur);
+        return DF_OK;
+    }
     SweepArgs a = sweep_args(h);
     HIP_OR(launch_halo_pack(a, h->rank > 0 ? h->send_l : nullptr, h->rank < h->world - 1 ? h->send_r : nullptr,
                             h->stream),
@@ -893,8 +981,8 @@ int phase_halo_rccl(df_handle *h)
     if (h->ghost) return DF_OK; // the y-pass filled the z-halo itself
     if (h->solo_strip) { // timing only: the pack, no exchange (or a hold of DFAMD_SOLO_XCHG_US in its place)
         int rc = phase_halo_pack(h);
-        if (!rc && h->solo_xchg_us > 0) HIP_OR(launch_hold(h->solo_xchg_us, h->stream), DF_EHIP);
-        if (!rc && h->gen_pending) HIP_OR(hipEventRecord(h->ev_xchg, h->stream), DF_EHIP);
+        if (!rc && h->solo_xchg_us > 0 && !h->tracing) HIP_OR(launch_hold(h->solo_xchg_us, h->stream), DF_EHIP);
+        if (!rc && h->gen_pending) Q_OR(q_record(h, h->ev_xchg, h->stream, h->gen_launched));
         return rc;
     }
     if (!h->comm) return fail(DF_EINVAL, "z-strip handle without an RCCL communicator: use df_filter_group");
@@ -960,6 +1048,10 @@ int phase_halo_zpass(df_handle *h, bool corr, bool sra, double dt)
 // part 0: every strip; 1: the halo-interior strips; 2: the edge strips around them (halo_interior)
 int phase_zpass(df_handle *h, bool corr, bool sra, double dt, int part, hipStream_t st)
 {
+    if (h->tracing) {
+        trace(h, TR_ZPASS, tr_stream(st ? st : h->stream), h->gen_used - 1, h->cur);
+        return DF_OK;
+    }
     SweepArgs a = sweep_args(h);
     if (part) {
         int lo = 0, hi = 0;
@@ -1426,6 +1518,7 @@ int ensure_comm_stream(df_handle *h)
 
 int ensure_ystream(df_handle *h)
 {
+    if (!h->ystream && h->yahead && h->tracing) h->ystream = (hipStream_t)(kTrStream + 2);
     if (h->ystream || !h->yahead || h->device < 0) return DF_OK;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     HIP_OR(hipStreamCreateWithFlags(&h->ystream, hipStreamNonBlocking), DF_EHIP);
@@ -1906,6 +1999,29 @@ int open_comm(df_handle *h, const df_config_c *cfg)
     return DF_OK;
 }
 
+// DF_DEVICE_TRACE: no GPU; stand-in streams and events, the state the create path would leave (the seed in state
+// slot 0, every release event recorded once on the stream)
+int open_trace(df_handle *h)
+{
+    h->device = -1;
+    h->tracing = true;
+    h->stream = (hipStream_t)(kTrStream + 0);
+    h->rng_stream = (hipStream_t)(kTrStream + 1);
+    for (int i = 0; i < 2; ++i) {
+        h->ev_rng[i] = (hipEvent_t)(kTrEvent + TE_RNG + i);
+        h->ev_swept[i] = (hipEvent_t)(kTrEvent + TE_SWEPT + i);
+    }
+    for (int k = 0; k < kMaxNoiseSets; ++k) h->ev_release[k] = (hipEvent_t)(kTrEvent + TE_RELEASE + k);
+    h->ev_counted = (hipEvent_t)(kTrEvent + TE_COUNTED);
+    h->ev_xchg = (hipEvent_t)(kTrEvent + TE_XCHG);
+    h->ev_halo = (hipEvent_t)(kTrEvent + TE_HALO);
+    h->dense_ready = h->gen_dense == 2 && h->geom.gen_split == 1;
+    if (int rc = ensure_ystream(h)) return rc;
+    trace(h, TR_STATE_W, -1, 0, 0);
+    for (int k = 0; k < kMaxNoiseSets; ++k) Q_OR(q_record(h, h->ev_release[k], h->stream, -(1ll << 40)));
+    return DF_OK;
+}
+
 int build(df_handle *h, const df_config_c *cfg)
 {
     int rc;
@@ -1940,10 +2056,14 @@ int build(df_handle *h, const df_config_c *cfg)
     // the halo exchange (one c4/8 rank with a 40 us stand-in exchange: 0.244 / 0.238 -> 0.215 / 0.210 ms, ranks
     // 0 / 4; 0.196-0.198 either way without it; profiles/r5/d/strip.jsonl)
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->yahead = 1;
-    // ahead handles hold three epochs of noise sets (consumed, swept ahead, generating)
+    // ahead handles hold three epochs of noise sets (consumed, swept ahead, generating), and so do batched
+    // single-GPU table planes (consumed and two generating; prefetch_epochs): their RNG chain competes with the
+    // sweeps for the same VALU slots, and a whole epoch of slack lets it fill the sweeps' gaps (same-box A/B of two
+    // builds, 60-call windows: c3 table 0.334-0.338 -> 0.327 ms, c2 table -2%; profiles/r5/r)
     h->hb_conf = h->hb;
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
-    if (h->yahead) h->nsets = 3 * h->hb;
+    if (h->yahead || (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb > 1))
+        h->nsets = 3 * h->hb;
     // z-strip handles in table mode, one process per GPU (split counting, the fused exchange): generations two
     // calls ahead. look is consulted only by fused_active() handles (one generation per hand-off), so in-process
     // groups and batched handles keep look 1 and the noise sets their batch needs (a batched handle
@@ -1951,6 +2071,7 @@ int build(df_handle *h, const df_config_c *cfg)
     if (h->world > 1 && h->coeff_mode == DF_COEFF_TABLE && (cfg->comm_id || h->solo_strip)) h->look = 2;
     if (h->hb > 1) h->look = 1;
     if (h->look == 2) h->nsets = std::max(h->nsets, 4);
+    if (cfg->device == DF_DEVICE_TRACE) return open_trace(h);
     if (cfg->device < 0) { // host-only handle: setup queries, no GPU
         h->device = -1;
         return DF_OK;
@@ -1983,6 +2104,10 @@ int step0(df_handle *h)
 void destroy(df_handle *h)
 {
     if (!h) return;
+    if (h->tracing) { // stand-in streams and events, nothing allocated
+        delete h;
+        return;
+    }
     // Drain every stream before any buffer or communicator goes: comm_stream may still hold a send/recv,
     // an unpack or the edge z-pass when a call failed part-way (phase_halo_zpass's error returns).
     if (h->stream) (void)hipStreamSynchronize(h->stream);
@@ -2080,6 +2205,10 @@ bool valid_dev(df_handle *h)
     return true;
 }
 
+// Handles the pipeline runs on: GPU handles and DF_DEVICE_TRACE handles (df_filter, the stream state, the hand-off
+// batch and the y-pass-ahead setting)
+bool valid_sched(df_handle *h) { return valid(h) && (h->tracing || valid_dev(h)); }
+
 // Handles whose results may be read. A DFAMD_SOLO_STRIP handle (tools/strip_timing.py: one rank of
 // a split plane timed alone, halo never exchanged) computes wrong fields by design.
 bool valid_out(df_handle *h)
@@ -2148,7 +2277,7 @@ df_handle *df_create(const df_config_c *cfg)
     else if (cfg->world > 1 && !cfg->comm_id && !(std::getenv("DFAMD_SOLO_STRIP") && std::atoi(std::getenv("DFAMD_SOLO_STRIP"))))
         rc = fail(DF_EINVAL, "world > 1 needs comm_id (RCCL) or df_create_group (in-process strips)");
     if (rc == DF_OK) rc = build(h, cfg);
-    if (rc == DF_OK && h->device >= 0) rc = step0(h);
+    if (rc == DF_OK && (h->device >= 0 || h->tracing)) rc = step0(h);
     if (rc != DF_OK) {
         std::string keep = g_err;
         destroy(h);
@@ -2163,12 +2292,12 @@ static int restart_pipeline(df_handle *h, int hb_new);
 
 int df_filter(df_handle *h, double dt)
 {
-    if (!valid_dev(h)) return DF_EINVAL;
+    if (!valid_sched(h)) return DF_EINVAL;
     int rc = check_rng_error(h);
     if (rc) return rc;
     if (h->world > 1 && !h->comm && !h->solo_strip)
         return fail(DF_EINVAL, "z-strip handle without RCCL: use df_filter_group");
-    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    if (!h->tracing) HIP_OR(hipSetDevice(h->device), DF_EHIP);
     if (h->hb != h->hb_conf && ++h->calls_since_load > kHbRestoreCalls) { // no state loads lately: batch again
         if ((rc = sync_all(h)) || (rc = restart_pipeline(h, h->hb_conf))) return rc;
     }
@@ -2457,6 +2586,14 @@ int df_get_coeffs(df_handle *h, int comp, int dir, double *out, long long n)
 
 int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
 {
+    if (h && h->tracing) {
+        trace(h, TR_SYNC);
+        trace(h, TR_STATE_R, -1, gen_set(h, h->gen_used), h->gen_used);
+        if (state) *state = 0;
+        if (saved_flag) *saved_flag = 0;
+        if (saved) *saved = 0;
+        return DF_OK;
+    }
     if (!valid_out(h)) return DF_EINVAL;
     HIP_OR(hipSetDevice(h->device), DF_EHIP);
     int rc = sync_all(h);
@@ -2489,15 +2626,19 @@ static int restart_pipeline(df_handle *h, int hb_new)
 
 int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
 {
-    if (!valid_dev(h)) return DF_EINVAL;
+    if (!valid_sched(h)) return DF_EINVAL;
     if (h->group) return fail(DF_EINVAL, "df_set_rng_state on a member of an in-process strip group");
-    HIP_OR(hipSetDevice(h->device), DF_EHIP);
+    if (!h->tracing) HIP_OR(hipSetDevice(h->device), DF_EHIP);
     int rc = sync_all(h);
     if (rc) return rc;
-    RngStateDev st{state, saved_flag ? 1 : 0, 0, saved};
-    HIP_OR(hipMemcpyAsync(h->rstate + gen_set(h, h->gen_used), &st, sizeof st, hipMemcpyHostToDevice, h->stream),
-           DF_EHIP);
-    HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    if (h->tracing) {
+        trace(h, TR_STATE_W, -1, gen_set(h, h->gen_used), h->gen_used);
+    } else {
+        RngStateDev st{state, saved_flag ? 1 : 0, 0, saved};
+        HIP_OR(hipMemcpyAsync(h->rstate + gen_set(h, h->gen_used), &st, sizeof st, hipMemcpyHostToDevice, h->stream),
+               DF_EHIP);
+        HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
+    }
     h->calls_since_load = 0;
     if (h->gen_launched > h->gen_used || h->hb != 1) // the prefetched noise came from the old state: redo it
         return restart_pipeline(h, 1);
@@ -2517,7 +2658,9 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
         {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap},
-        {"halo_ghost", h->ghost}};
+        {"halo_ghost", h->ghost},
+        // read-only: noise sets allocated at create, epochs generated ahead of the one consumed (prefetch_epochs)
+        {"noise_sets", h->nsets}, {"prefetch_epochs", prefetch_epochs(h)}};
     for (const auto &kv : keys)
         if (k == kv.first) {
             *value = kv.second;
@@ -2571,7 +2714,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             return fail(DF_EINVAL, "halo_ghost needs a table-mode z-strip handle with row-uniform half-widths");
         if ((value != 0) != (h->ghost != 0)) {
             std::vector<df_handle *> mem = h->group ? *h->group : std::vector<df_handle *>{h};
-            if (h->device >= 0)
+            if (h->device >= 0 || h->tracing)
                 for (df_handle *m : mem) // queued generations and sweeps keep the layout they had
                     if (int rc = sync_all(m)) return rc;
             h->ghost = value != 0;
@@ -2580,7 +2723,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
             // once, so once all its strips agree)
             bool agree = true;
             for (df_handle *m : mem) agree = agree && m->ghost == h->ghost;
-            if (h->device >= 0 && agree && h->gen_launched > h->gen_used) {
+            if ((h->device >= 0 || h->tracing) && agree && h->gen_launched > h->gen_used) {
                 if (!h->group) {
                     if (int rc = restart_pipeline(h, h->hb)) return rc;
                 } else {
@@ -2638,7 +2781,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value > 1 && (h->world > 1 || h->comm || h->group))
             return fail(DF_EINVAL, "handoff_batch > 1 is for single-GPU handles");
         h->hb_conf = value;
-        if (h->device >= 0 && value != h->hb) {
+        if ((h->device >= 0 || h->tracing) && value != h->hb) {
             int rc = sync_all(h);
             if (rc) return rc;
             if ((rc = restart_pipeline(h, value))) return rc;
@@ -2754,6 +2897,17 @@ int df_gather_field(df_handle *h, int which, long long n, const long long *plane
 }
 
 void *df_stream(df_handle *h) { return valid_dev(h) ? (void *)h->stream : nullptr; }
+
+long long df_trace(df_handle *h, long long *out, long long cap)
+{
+    if (!valid(h) || !h->tracing) {
+        fail(DF_EINVAL, "df_trace needs a handle created with device = DF_DEVICE_TRACE");
+        return -1;
+    }
+    const long long n = (long long)h->tr.size() / 6;
+    if (out) std::memcpy(out, h->tr.data(), (size_t)std::min(n, std::max(0ll, cap)) * 6 * sizeof(long long));
+    return n;
+}
 
 int df_get_noise(df_handle *h, int comp, int dir, double *out, long long n)
 {

@@ -19,6 +19,7 @@ DATA = os.path.join(HERE, "data")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "df_c.h")
 
 PLANE = {"native": 0, "synthetic": 1, "grid": 2}
+DEVICE_TRACE = -2  # df_c.h DF_DEVICE_TRACE: the noise pipeline's host logic, recorded instead of run (df_trace)
 COEFF = {"packed": 0, "table": 1}
 FIELDS = {"u": 0, "v": 1, "w": 2, "T": 3, "rho": 4, "filt_old_u": 5, "filt_old_v": 6, "filt_old_w": 7,
           "filt_u": 8, "filt_v": 9, "filt_w": 10}
@@ -120,6 +121,7 @@ def lib():
         "df_algorithmic_bytes": (C.c_double, [H, C.c_int]),
         "df_comm_unique_id": (C.c_int, [C.c_void_p, C.c_size_t]),
         "df_comm_info": (C.c_int, [H, C.POINTER(CommStats)]),
+        "df_trace": (C.c_longlong, [H, C.c_void_p, C.c_longlong]),
         "df_destroy": (None, [H]),
     }
     for name, (res, args) in sig.items():
@@ -256,6 +258,16 @@ class DigitalFilter:
     def wait(self):
         """This handle's results so far (df_wait), not the later calls' noise already queued."""
         _check(lib().df_wait(self._h))
+
+    def trace(self):
+        """Schedule records of a device=DEVICE_TRACE handle (df_trace): int64 array (n, 6) {op, stream, a, b, c, d}."""
+        n = lib().df_trace(self._h, None, 0)
+        if n < 0:
+            raise DFError(lib().df_last_error().decode())
+        out = np.zeros((n, 6), dtype=np.int64)
+        if n:
+            lib().df_trace(self._h, out.ctypes.data, n)
+        return out
 
     # --- stage API (df.hpp:96-101)
     def generate_white_noise(self):

@@ -72,7 +72,8 @@ typedef struct df_config_c {
     int coeff_mode;                        /* enum df_coeff_mode */
     const char *csv_path;                  /* non-NULL: write the reference CSV after every df_filter (df.cpp:466-467) */
     int device;                            /* HIP device ordinal; -1 = host-only handle (setup
-                                              queries only, no GPU: used by CPU tests) */
+                                              queries only, no GPU: used by CPU tests); DF_DEVICE_TRACE
+                                              = schedule trace (df_trace) */
     int rank, world;                       /* z-strip partition: this GPU is strip `rank` of `world` */
     const void *comm_id;                   /* 128-byte RCCL unique id, from df_comm_unique_id (world > 1;
                                               world 1 also accepted: exercises the same RCCL calls) */
@@ -88,6 +89,15 @@ typedef struct df_config_c {
 } df_config_c;
 
 typedef struct df_handle df_handle;
+
+/* df_config_c.device of a schedule-trace handle: no GPU. df_create, df_filter, df_set_rng_state, df_rng_state and
+ * df_set_tuning("handoff_batch" | "ypass_ahead") run the host logic of the noise pipeline - generations, hand-off
+ * epochs, the y-pass ahead, releases, restarts - and record what each would enqueue instead of calling HIP;
+ * df_trace copies the records out (tests/test_schedule.py checks them). */
+#define DF_DEVICE_TRACE (-2)
+/* Records of a DF_DEVICE_TRACE handle so far, six int64 each {op, stream, a, b, c, d} (df_capi.cpp TraceOp);
+ * copies min(cap, n) of them into out (NULL: count only) and returns n, or -1. */
+long long df_trace(df_handle *h, long long *out, long long cap);
 
 typedef struct df_profile {
     long long calls;      /* df_filter calls timed since df_set_profiling(h, 1) */
@@ -245,7 +255,8 @@ int df_set_tuning(df_handle *h, const char *key, int value);
 
 /* The launch shape the handle will use for a df_set_tuning key: the plane-dependent defaults chosen at
  * create time (host-only handles included) or the last setting. Every df_set_tuning key but
- * "halo_loopback"; DF_EINVAL for other keys. */
+ * "halo_loopback", and two read-only keys of the noise pipeline: "noise_sets" (sets allocated at create) and
+ * "prefetch_epochs" (hand-off epochs generated ahead of the one being consumed); DF_EINVAL for other keys. */
 int df_get_tuning(df_handle *h, const char *key, int *value);
 
 /* Timing (hipEvents on the handle's stream). on = 0 off, 1 events on every df_filter, n > 1 on every

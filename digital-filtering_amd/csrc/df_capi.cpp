@@ -1281,6 +1281,14 @@ int build_ylists(df_handle *h)
     return rc;
 }
 
+// ypass_t64 addresses each component's r_ys (with its kYTailRows) by 32-bit byte offsets
+bool t64_fits(const df_handle *h)
+{
+    int nyp = 0;
+    for (int c = 0; c < 3; ++c) nyp = std::max(nyp, h->setup.comp[c].Ny_max);
+    return (double)(h->Ny + 2 * nyp + kYTailRows) * h->Pzy * 8.0 < 4294967296.0;
+}
+
 // This handle's z-strip of the plane, its launch shapes and its share of the coefficient stream.
 int plan_strips(df_handle *h)
 {
@@ -1392,6 +1400,7 @@ int plan_strips(df_handle *h)
         h->nstrips_g = (h->Wext + kStrip - 1) / kStrip;
         h->Pzy = std::max(h->Pz, h->nstrips_g * kStrip);
     }
+    if (h->ylds == 3 && !t64_fits(h)) h->ylds = 2; // ypass_t64 addresses r_ys with 32-bit offsets
 
     // Write windows (SweepArgs::ywin_T): on planes whose sweeps stream >= 2 GB of packed coefficients per
     // pass the waves hold their stores for a chip-wide window of 2.56 us every 41 us; c3 -5.1% per call,
@@ -1607,7 +1616,7 @@ int alloc_components(df_handle *h)
         CompDev &d = h->c[c];
         const ComponentSetup &F = s.comp[c];
         for (int set = 0; set < h->nsets; ++set) {
-            if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp) * h->Pzy))) return rc;
+            if ((rc = dalloc_t(h, &d.ry[set], (size_t)(Ny + 2 * d.Nyp + kYTailRows) * h->Pzy))) return rc;
             if ((rc = dalloc_t(h, &d.rz[set], (size_t)Ny * d.rz_pitch))) return rc;
         }
         if ((rc = dalloc_t(h, &d.filt_old, n_loc))) return rc;
@@ -2691,6 +2700,7 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
+        if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {
         if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");

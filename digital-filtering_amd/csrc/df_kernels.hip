@@ -1800,8 +1800,14 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 // chunk's R x C coefficients (uniform: one scalar window per row, zero taps where the window hangs past the
 // row's range) are therefore loaded before the chunk's barrier, whose wait they share, and the chunk's sums
 // then wait on LDS reads alone; no chunk takes a per-tap path (a scalar load and its wait per tap made a
-// row's first and last chunk cost more than the rest of it). The noise loads of the chunks in flight go to
-// clamped rows instead of being predicated, so their vmcnt waits are counted, not zero.
+// row's first and last chunk cost more than the rest of it). The noise loads of the chunks in flight are
+// unconditional, so their vmcnt waits are counted, not zero.
+// Round 6 (1.45 scalar instructions per vector one, the CU's one scalar unit busier than
+// the FP64 pipe): the per-chunk bookkeeping is all increments. Each noise load has its own lane pointer advanced
+// by one chunk per step (one VALU add, where a clamped row index cost four scalar instructions per load: r_ys
+// now carries kYTailRows rows past its last so the loads need no clamp; rows past a block's range are summed
+// with zero taps or never staged); each row's coefficient window is a scalar pointer advanced by C doubles, and
+// whether the row has a tap in the chunk is a compare of the chunk index against a range fixed at the start.
 // Each row adds its taps in the order i = -N..N (noise rows ascending) with df.cpp:373-375's products:
 // bit-identical to every other form.
 template <int R, int NW, int C, int PD>
@@ -1826,29 +1832,40 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         mhi = max(mhi, j0 + q + N);
     }
     const int jw = j0 + w * R;
-    int lo[R], hi[R];
-    const double *tb[R]; // row r's full tap vector: tap t = m - lo[r] at tb[r][t]
+    // row r has a tap in chunk i (rows mlo + C i ..) for i - ilo[r] in [0, iw[r]] (unsigned: one compare); its
+    // window there is cwin[r] + C i
+    int ilo[R];
+    unsigned iw[R];
+    const double *cwin[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        lo[r] = 1 << 30;
-        hi[r] = -(1 << 30);
-        tb[r] = a.tabf;
+        ilo[r] = 1 << 30; // no row: i - ilo is negative, far above iw as unsigned
+        iw[r] = 0;
+        cwin[r] = a.tabf;
         if (jw + r < Ny) {
-            const int N = nst[jw + r];
-            lo[r] = jw + r - N;
-            hi[r] = jw + r + N;
-            tb[r] = a.tabf + a.tabf_off[N];
+            const int N = nst[jw + r], lo = jw + r - N;
+            ilo[r] = (lo - mlo) / C; // lo >= mlo
+            iw[r] = (unsigned)((jw + r + N - mlo) / C - ilo[r]);
+            cwin[r] = a.tabf + a.tabf_off[N] + (mlo - lo); // tap t = m - lo of noise row m at tabf_off[N] + t
         }
     }
     const int col = ct * 64 + lane; // < Pz: a padding column is loaded and summed but never stored
-    const double *np = a.ry[c] + (size_t)a.Nyp[c] * a.Pz + col; // noise row m at np + m * Pz
+    // The next chunk each of this wave's loads fetches: rows 2 (w + NW k) and + 1 of it, at byte offset vo[k] of
+    // this lane's column from the uniform bases nb (even rows) and nb1 (odd rows): global loads with a scalar base
+    // and a 32-bit vector offset (launch_ypass_t checks r_ys < 4 GiB), one vector add per pair and chunk.
+    const unsigned Pz8 = (unsigned)a.Pz * 8u;
+    const char *nb = reinterpret_cast<const char *>(a.ry[c]), *nb1 = nb + Pz8;
+    unsigned vo[LP];
+#pragma unroll
+    for (int k = 0; k < LP; ++k) vo[k] = (unsigned)(a.Nyp[c] + mlo + 2 * (w + NW * k)) * Pz8 + (unsigned)col * 8u;
     dvec2 pre[PD][LP]; // wave w loads row pairs w + NW k of the chunk
-    auto gload = [&](auto K, int u0) {
+    auto gload = [&](auto K) {
         constexpr int k0 = decltype(K)::value;
 #pragma unroll
         for (int k = 0; k < LP; ++k) {
-            const int m = u0 + 2 * (w + NW * k);
-            pre[k0][k] = dvec2{np[(ptrdiff_t)min(m, mhi) * a.Pz], np[(ptrdiff_t)min(m + 1, mhi) * a.Pz]};
+            pre[k0][k] = dvec2{*reinterpret_cast<const double *>(nb + vo[k]),
+                               *reinterpret_cast<const double *>(nb1 + vo[k])};
+            vo[k] += (unsigned)C * Pz8;
         }
     };
     auto lstore = [&](auto K, int buf) {
@@ -1856,22 +1873,25 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 #pragma unroll
         for (int k = 0; k < LP; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
     };
-    // Every chunk takes the whole-window path: a row's window may hang past its first or last tap into the
-    // table's zero guards (kTabGuard >= C, df_capi.cpp upload_tables), and a row with no tap in the chunk reads
-    // the zeros at the table's start; zero taps leave each sum bit for bit.
-    auto live = [&](int u0) { // some row of the wave has a tap in the chunk
+    // Every live chunk takes the whole-window path: a row's window may hang past its first or last tap into the
+    // table's zero guards (kTabGuard >= C, df_capi.cpp upload_tables); zero taps leave each sum bit for bit.
+    bool liv[R];
+    auto live = [&](int i) {
         bool f = false;
 #pragma unroll
-        for (int r = 0; r < R; ++r) f = f || (lo[r] <= u0 + C - 1 && hi[r] >= u0);
+        for (int r = 0; r < R; ++r) {
+            liv[r] = (unsigned)(i - ilo[r]) <= iw[r];
+            f = f || liv[r];
+        }
         return f;
     };
-    double cw[R][C]; // the chunk's coefficients (uniform)
-    auto cload = [&](double (&dst)[R][C], int u0) {
+    double cw[R][C]; // the chunk's coefficients (uniform), loaded whether or not the chunk is live (no branch)
+    auto cload = [&](int i) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const double *src = lo[r] <= u0 + C - 1 && hi[r] >= u0 ? tb[r] + (u0 - lo[r]) : a.tabf;
+            const double *src = liv[r] ? cwin[r] + i * C : a.tabf; // a.tabf: kTabGuard zeros
 #pragma unroll
-            for (int q = 0; q < C; ++q) dst[r][q] = src[q];
+            for (int q = 0; q < C; ++q) cw[r][q] = src[q];
         }
     };
     double acc[R];
@@ -1892,28 +1912,26 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     // ypass_tlds_kernel); its coefficients (full chunks) loaded before the barrier that precedes it
     const int nch = (mhi - mlo) / C + 1;
     // prologue: chunks 0 .. PD - 1 in flight, chunk 0 staged
-    unroll_to<0, PD>([&](auto K) { gload(K, mlo + decltype(K)::value * C); });
+    unroll_to<0, PD>([&](auto K) { gload(K); });
     lstore(ic_t<0>{}, 0);
-    bool on = live(mlo);
-    if (on) cload(cw, mlo);
+    bool on = live(0);
+    cload(0);
     __syncthreads();
+    // Steps run in whole groups of PD: a step past the last chunk stages rows no row has a tap in (on is false
+    // from there: every ilo + iw < nch) and sums nothing. Its loads reach at most 2 PD C - 1 rows past the block's
+    // last (<= 127 < kYTailRows).
     auto step = [&](auto K, int i) {
         constexpr int k = decltype(K)::value;
-        // chunk i + PD into the set chunk i left - unconditionally (rows clamped to mhi past the end), so the
-        // count of loads in flight is fixed and the waits below are counted vmcnt(n), not vmcnt(0)
-        gload(K, mlo + (i + PD) * C);
+        // chunk i + PD into the set chunk i left - unconditionally, so the count of loads in flight is fixed and
+        // the waits below are counted vmcnt(n), not vmcnt(0)
+        gload(K);
         compute(i & 1, on);
-        if (i + 1 < nch) {
-            lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
-            on = live(mlo + (i + 1) * C);
-            if (on) cload(cw, mlo + (i + 1) * C);
-        }
+        lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+        on = live(i + 1);
+        cload(i + 1);
         __syncthreads();
     };
-    for (int i = 0; i < nch; i += PD)
-        unroll_to<0, PD>([&](auto K) {
-            if (i + decltype(K)::value < nch) step(K, i + decltype(K)::value);
-        });
+    for (int i = 0; i < nch; i += PD) unroll_to<0, PD>([&](auto K) { step(K, i + decltype(K)::value); });
     if (col < a.ylo[c] || col >= a.yhi[c]) return;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1929,6 +1947,8 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
     if constexpr (TABLE) {
         if (a.ylds == 3 && !a.per_cell) { // 64-column tiles, heaviest first; rows per wave from ylist_R
             const dim3 grid((unsigned)a.ylist_n);
+            for (int c = 0; c < 3; ++c) // 32-bit byte offsets into r_ys (df_capi.cpp t64_fits)
+                if ((double)(a.Ny + 2 * a.Nyp[c] + kYTailRows) * a.Pz * 8.0 >= 4294967296.0) return hipErrorInvalidValue;
             // R x C coefficients of a chunk held in SGPRs (24 doubles at most: more spill)
             // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 1 x 24 26.6 (the call beside the
             // RNG -2%, profiles/r5/p), 2 x 16 26.6, 2 x 8 35-39, the round-4 ypass_tlds 40.4; 4 chunks in flight lose

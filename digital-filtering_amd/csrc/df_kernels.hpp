@@ -24,6 +24,8 @@ namespace dfamd {
 
 constexpr int kStrip = 128;           // cells per strip (one wave, 2 per lane)
 constexpr int kMaxNoiseSets = 12;     // noise sets per handle (2 x the hand-off batch; 3 x with the y-pass ahead)
+constexpr int kYTailRows = 128;       // r_ys rows allocated past the last noise row: ypass_t64 loads whole chunks
+                                      // up to (yt_pd + 1) * yt_chunk <= 96 rows past a block's last row, unclamped
 constexpr int kRngThreads = 256;      // threads per RNG block
 constexpr int kRngPerThread = 16;     // polar attempts per thread
 constexpr int kRngBlockAttempts = kRngThreads * kRngPerThread;

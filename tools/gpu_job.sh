@@ -14,7 +14,14 @@
 #   rocpy=SCRIPT[,ARGS]       rocprofv3 --kernel-trace --stats -- python3 SCRIPT ARGS       400 s
 #   sh=SCRIPT[,ARGS]          bash SCRIPT ARGS (a tools/ script)                           400 s
 #   smoke                     __graft_entry__.smoke()                                      300 s
-# Outputs: gpurun_out/TAG/<i>_<step>.{log,json}.
+#   ab=CFG,MODE,A,B[,ROUNDS]  tools/ab.py one-handle A/B of tunings A vs B (k=v, several joined by +), 60-call
+#                             windows, 24 untimed calls after each switch, wall only -> ab.jsonl           300 s
+#   trace=PLANE,MODE,CALLS[,k=v ...]  rocprofv3 kernel trace of tools/plane_loop.py with the RNG on the sweep
+#                             stream (DFAMD_RNG_OVERLAP=0: every kernel timed alone) -> split.csv          200 s
+#   pmc=PLANE,MODE,CALLS[,k=v ...]    tools/pmc_plane.sh: SQ counter passes + a kernel trace -> pmc.json  600 s
+#   final                     the closing run: tests, smoke, bench, rocprofv3 of the bench (as four steps)
+# Outputs: gpurun_out/TAG/<i>_<step>.{log,json}. Every earlier one-off tools/job_*.sh is one line of these steps
+# (tools/README.md, "Recipes").
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -22,8 +29,12 @@ TAG=$1; shift
 O=$ROOT/gpurun_out/$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
-i=0
+steps=()
 for step in "$@"; do
+  if [ "$step" = final ]; then steps+=(tests smoke bench prof=--cpu-baseline,off); else steps+=("$step"); fi
+done
+i=0
+for step in "${steps[@]}"; do
   i=$((i + 1))
   name=${step%%=*}
   arg=""
@@ -53,6 +64,18 @@ for step in "$@"; do
     sh) set -- $arg; script=$1; shift
         timeout -k 10 400 bash "$script" "$@" > "$base.log" 2>&1; rc=$?; tail -30 "$base.log" ;;
     smoke) timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$base.log" 2>&1; rc=$?; tail -2 "$base.log" ;;
+    ab) set -- $arg
+        timeout -k 10 300 python3 tools/ab.py --config $1 --mode $2 --rounds ${5:-7} --calls 60 --switch-calls 24 \
+          --events 0 --tune-a "${3//+/,}" --tune-b "${4//+/,}" >> "$O/ab.jsonl" 2> "$base.log"; rc=$?
+        [ $rc -eq 0 ] && tail -1 "$O/ab.jsonl" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); \
+print(d['config'], d['mode'], 'A', d['A'], d['A_median_ms']['wall_ms'], '| B', d['B'], d['B_median_ms']['wall_ms'])" ;;
+    trace) set -- $arg; plane=$1; mode=$2; calls=$3; shift 3
+        (cd /tmp && DFAMD_RNG_OVERLAP=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv \
+           -d "$base.d" -o run -- python3 "$ROOT/tools/plane_loop.py" $plane $mode $calls "$@" > "$base.log" 2>&1); rc=$?
+        [ $rc -eq 0 ] && python3 tools/rocprof_split.py "$base.d/run_kernel_trace.csv" > "$base.split.csv" && \
+          grep -E "ypass|zpass|rng_" "$base.split.csv" | head -8 ;;
+    pmc) set -- $arg
+        PMC_TAG=_$i timeout -k 10 600 bash tools/pmc_plane.sh "$@" > "$base.log" 2>&1; rc=$?; tail -12 "$base.log" ;;
     *) echo "unknown step $name"; exit 2 ;;
   esac
   if [ $rc -ne 0 ]; then

@@ -384,11 +384,13 @@ def cpu_baseline_parallel(args, Ny, N_min, N_max):
 
 
 def dropin_timing(args):
-    """The C++ drop-in's per-call cost: examples/cpp-test `time` runs, on one object,
-    the C-ABI call (df_filter + df_sync) and DIGITAL_FILTER::filter() with host_mirror 0 (no host
-    copies), 1 (default: u/v/w.fluc, T', rho' - one sync, page-locked vectors) and 2 (also filt_old and
-    filt), on the reference's grid and on c3, in both coefficient modes. The mirror refresh is a PCIe
-    D2H transfer of 5 (or 8) fields; `mirror1_GBps` is its rate."""
+    """The C++ drop-in's per-call cost: examples/cpp-test `time` runs, on one
+    object, the C-ABI call with the per-step wait a synchronous caller makes (df_filter + df_wait: this call's
+    fields; `capi_sync_all_ms`: + df_sync, which also waits for later calls' noise and y-passes), the same with
+    the y-pass-ahead setting flipped, and DIGITAL_FILTER::filter() with host_mirror 0 (no host copies; also
+    stream-ordered, no host wait), 1 (default: u/v/w.fluc, T', rho' - one sync, page-locked vectors) and 2
+    (also filt_old and filt), on the reference's grid and on c3, in both coefficient modes. The mirror refresh
+    is a PCIe D2H transfer of 5 (or 8) fields; `mirror1_GBps` is its rate."""
     exe = os.path.join(ROOT, "examples", "cpp-test")
     if not os.path.exists(exe):
         return {"error": "examples/cpp-test not built (make -C examples)"}
@@ -904,6 +906,16 @@ def main(argv=None):
     rank_phase("reports (drop-in, CPU baseline, JSON line)")
     if ctx.rank == 0 and ctx.world == 1 and args.dropin == "auto":
         dropin = dropin_timing(args)
+        nd = dropin.get("native/table", {})
+        if "native_table" in others and "capi_ms" in nd:
+            # the drop-in default's per-step cost on the reference's grid, beside its async figure:
+            # df_filter + df_wait (this call's fields only), + df_sync (later calls' noise too), and the C++ filter()
+            others["native_table"]["synchronous_call"] = {
+                "capi_ms": nd["capi_ms"], "capi_sync_all_ms": nd.get("capi_sync_all_ms"),
+                "dropin_mirror0_ms": nd["dropin_ms"]["mirror0"],
+                "dropin_stream_ordered_ms": nd["dropin_ms"].get("mirror0_stream_ordered"),
+                "ypass_ahead": nd.get("ypass_ahead"), "capi_ms_ypass_ahead_flipped": nd.get("capi_ms_ypass_ahead_flipped"),
+                "note": "examples/cpp-test time, 60 calls each: a synchronous caller's wall per step"}
     if ctx.rank == 0:
         cpu = cpu_par = None
         if args.cpu_baseline == "auto" and ctx.world == 1 and wl["plane"] != "native":

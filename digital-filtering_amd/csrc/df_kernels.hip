@@ -1911,6 +1911,11 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
     // ypass_tlds_kernel); its coefficients (full chunks) loaded before the barrier that precedes it
     const int nch = (mhi - mlo) / C + 1;
+    // The longest blocks set the kernel's time: once the short ones around them have drained, a CU holds one
+    // such block (a wave per SIMD), whose serial chunk chain then runs at one wave's latency. Raising their waves'
+    // issue priority makes them progress at that pace from the start, the short blocks filling the issue slots
+    // they leave (SweepArgs::ylist_prio; results unchanged).
+    if (a.ylist_prio > 0 && nch >= a.ylist_prio) __builtin_amdgcn_s_setprio(3);
     // prologue: chunks 0 .. PD - 1 in flight, chunk 0 staged
     unroll_to<0, PD>([&](auto K) { gload(K); });
     lstore(ic_t<0>{}, 0);

@@ -219,6 +219,7 @@ struct df_handle {
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
     int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
     int yt_prio = 0; // ypass_t64: blocks of at least this many chunks run their waves at raised issue priority
+    int sweep_prio = 0; // issue priority (0-3) of the sweep kernels' waves beside the noise generation
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
@@ -405,6 +406,7 @@ SweepArgs sweep_args(df_handle *h)
     a.ylist_C = h->yt_chunk;
     a.ylist_PD = h->yt_pd;
     a.ylist_prio = h->yt_prio;
+    a.sweep_prio = h->sweep_prio;
     for (int c = 0; c < 3; ++c) {
         a.yout[c] = h->c[c].Nzp;
         a.ylo[c] = 0;
@@ -2664,7 +2666,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"yt_prio", h->yt_prio}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
+        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"yt_prio", h->yt_prio}, {"sweep_prio", h->sweep_prio}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2704,6 +2706,9 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
+    } else if (k == "sweep_prio") {
+        if (value < 0 || value > 3) return fail(DF_EINVAL, "sweep_prio must be 0-3");
+        h->sweep_prio = value;
     } else if (k == "yt_prio") {
         if (value < 0) return fail(DF_EINVAL, "yt_prio must be >= 0 (0: off)");
         h->yt_prio = value;

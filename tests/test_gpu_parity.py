@@ -324,7 +324,8 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
-                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1)]
+                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1),
+                dict(sweep_prio=2), dict(sweep_prio=0)]
     if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back
         settings += [dict(ylds=3, yt_rows=1), dict(yt_rows=2), dict(yt_chunk=8), dict(yt_rows=1, yt_pd=4), dict(yt_pd=2),
                      dict(yt_chunk=24),

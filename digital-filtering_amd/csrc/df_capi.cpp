@@ -218,8 +218,6 @@ struct df_handle {
     int cur = 0;                // noise set of the current step
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
     int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
-    int yt_prio = 0; // ypass_t64: blocks of at least this many chunks run their waves at raised issue priority
-    int sweep_prio = 0; // issue priority (0-3) of the sweep kernels' waves beside the noise generation
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
@@ -405,8 +403,6 @@ SweepArgs sweep_args(df_handle *h)
     a.ylist_R = h->yt_rows;
     a.ylist_C = h->yt_chunk;
     a.ylist_PD = h->yt_pd;
-    a.ylist_prio = h->yt_prio;
-    a.sweep_prio = h->sweep_prio;
     for (int c = 0; c < 3; ++c) {
         a.yout[c] = h->c[c].Nzp;
         a.ylo[c] = 0;
@@ -1330,6 +1326,10 @@ int plan_strips(df_handle *h)
         // tiles, one cell and one row per lane, heaviest blocks first, whole-window chunks: 40.4 -> 24.7 us alone,
         // profiles/r5). c3 and c2 (short chains, FP64-issue-bound) lose with LDS staging.
         if (h->coeff_mode == DF_COEFF_TABLE && long_chain) h->ylds = s.per_cell ? 2 : 3;
+        // ypass_t64 at 2 rows per wave (round 6): with the per-chunk bookkeeping down to increments, two rows' chains
+        // per lane beat one on two boxes (kernel alone -9% and -11%, call -7%; profiles/r6/d, e); round 5's form
+        // lost with 2 (its scalar bookkeeping, 1.45 scalar instructions per vector one, was the bottleneck)
+        if (h->ylds == 3) h->yt_rows = 2;
         // Long chains, packed: one block per row pair, noise loads shared by both rows, the next chunk in
         // flight, XCD runs of equal bytes (the reference's grid: y-pass 0.209 (one wave per tile) -> 0.181
         // (one block per tile) -> 0.157 ms; profiles/r2/ab_ycoop_native.jsonl, ab_ycoop2_native.jsonl).
@@ -2666,7 +2666,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"yt_prio", h->yt_prio}, {"sweep_prio", h->sweep_prio}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
+        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2706,12 +2706,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
-    } else if (k == "sweep_prio") {
-        if (value < 0 || value > 3) return fail(DF_EINVAL, "sweep_prio must be 0-3");
-        h->sweep_prio = value;
-    } else if (k == "yt_prio") {
-        if (value < 0) return fail(DF_EINVAL, "yt_prio must be >= 0 (0: off)");
-        h->yt_prio = value;
     } else if (k == "yt_pd") {
         if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
         if (value == 4 && (h->yt_rows != 1 || h->yt_chunk != 16))

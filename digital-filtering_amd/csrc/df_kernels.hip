@@ -21,14 +21,6 @@ namespace dfamd {
 
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// SweepArgs::sweep_prio > 0: the sweeps' waves issue at that priority (s_setprio), ahead of the noise generation
-// of later calls co-running on the other stream, which then fills the issue slots they leave (results unchanged)
-__device__ __forceinline__ void sweep_priority(const SweepArgs &a)
-{
-    if (a.sweep_prio == 1) __builtin_amdgcn_s_setprio(1);
-    else if (a.sweep_prio == 2) __builtin_amdgcn_s_setprio(2);
-    else if (a.sweep_prio >= 3) __builtin_amdgcn_s_setprio(3);
-}
 
 typedef double dvec2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(3))) dvec2 *lds_pair_ptr; // LDS-staged noise (ds_read_b128)
@@ -1182,7 +1174,6 @@ __device__ __forceinline__ void write_window(int T, int W)
 template <int R, bool TABLE, bool NT, int YU, bool PC>
 __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 {
-    sweep_priority(a);
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
     const int lane = threadIdx.x & 63;
@@ -1350,7 +1341,6 @@ __global__ __launch_bounds__(256) void ypass_kernel(SweepArgs a, int nrowblk)
 template <int R, int KYD>
 __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowblk)
 {
-    sweep_priority(a);
     const int c = blockIdx.y;
     if (!((a.comps_mask >> c) & 1)) return;
     const int lane = threadIdx.x & 63;
@@ -1530,7 +1520,6 @@ __global__ __launch_bounds__(256) void ypass_table_kernel(SweepArgs a, int nrowb
 template <bool NT, int KPW>
 __global__ __launch_bounds__(256) void ypass_coop2_kernel(SweepArgs a)
 {
-    sweep_priority(a);
     constexpr int CH = 4 * KPW; // noise rows per chunk and tap group
     constexpr int RR = 2, RH = 1; // rows per block, rows summed per thread
     __shared__ double2 prod[RR * CH * 64];
@@ -1674,7 +1663,6 @@ template <int K, int E, class F> __device__ __forceinline__ void unroll_to(F &&f
 template <int R, int PD, int NW = 4, int C = 16>
 __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nrowblk)
 {
-    sweep_priority(a);
     constexpr int LW = C / NW; // chunk rows each wave loads
     __shared__ double2 nbuf[2][C][64];
     const int c = blockIdx.y;
@@ -1826,7 +1814,6 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 template <int R, int NW, int C, int PD>
 __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 {
-    sweep_priority(a);
     constexpr int LP = C / (2 * NW); // pairs of chunk rows each wave loads
     static_assert(C % (2 * NW) == 0, "chunk row pairs split evenly over the waves");
     // noise rows 2p, 2p + 1 of a chunk side by side for each lane: one ds_read_b128 (4 LDS cycles for 1 KiB)
@@ -1925,11 +1912,6 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
     // ypass_tlds_kernel); its coefficients (full chunks) loaded before the barrier that precedes it
     const int nch = (mhi - mlo) / C + 1;
-    // The longest blocks set the kernel's time: once the short ones around them have drained, a CU holds one
-    // such block (a wave per SIMD), whose serial chunk chain then runs at one wave's latency. Raising their waves'
-    // issue priority makes them progress at that pace from the start, the short blocks filling the issue slots
-    // they leave (SweepArgs::ylist_prio; results unchanged).
-    if (a.ylist_prio > 0 && nch >= a.ylist_prio) __builtin_amdgcn_s_setprio(3);
     // prologue: chunks 0 .. PD - 1 in flight, chunk 0 staged
     unroll_to<0, PD>([&](auto K) { gload(K); });
     lstore(ic_t<0>{}, 0);
@@ -2088,7 +2070,6 @@ __device__ __forceinline__ void zstage_copy(const SweepArgs &a, double *lds, int
 template <bool TABLE, bool NT, int ZU, bool PC, bool SPLIT = false>
 __global__ __launch_bounds__(256) void zpass_kernel(SweepArgs a)
 {
-    sweep_priority(a);
     extern __shared__ double zstage_lds[]; // 3 x zstage_reg doubles when a.zstage (table mode)
     const int lane = threadIdx.x & 63;
     const int Ny = a.Ny, nst = a.zs_n; // this launch's strips (SweepArgs::zs_lo ...)

@@ -154,8 +154,6 @@ struct SweepArgs {
     const int *ylist;
     int ylist_n, ylist_nrb, ylist_ncol, ylist_R, ylist_C, ylist_PD; // R rows per wave, C noise rows per LDS chunk,
                                                                      // PD chunks of noise loads in flight
-    int ylist_prio; // > 0: a block of at least ylist_prio chunks raises its waves' issue priority (s_setprio)
-    int sweep_prio; // 0-3: the issue priority of every sweep kernel's waves (s_setprio; 0 = the default)
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

@@ -194,8 +194,7 @@ def test_golden_native_grid(mode, tuning):
                                          ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
                                          ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
                                          ("table", dict(ylds=3, yt_pd=4)), ("table", dict(ylds=3, yt_rows=2, yt_chunk=8)),
-                                         ("table", dict(ylds=3, yt_chunk=24)), ("table", dict(ylds=3, yt_prio=8)),
-                                         ("table", dict(ylds=3, yt_rows=2, yt_prio=1)),
+                                         ("table", dict(ylds=3, yt_chunk=24)),
                                          ("table", dict(ylds=0))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
@@ -324,12 +323,11 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
-                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1),
-                dict(sweep_prio=2), dict(sweep_prio=0)]
+                dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1)]
     if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back
         settings += [dict(ylds=3, yt_rows=1), dict(yt_rows=2), dict(yt_chunk=8), dict(yt_rows=1, yt_pd=4), dict(yt_pd=2),
                      dict(yt_chunk=24),
-                     dict(yt_rows=2, yt_chunk=16), dict(yt_prio=2), dict(yt_prio=0), dict(ylds=2), dict(ylds=0)]
+                     dict(yt_rows=2, yt_chunk=16), dict(ylds=2), dict(ylds=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

@@ -329,7 +329,7 @@ def test_alloc_registry_rejects_overlapping_ranges():
 @pytest.mark.parametrize("plane,mode,expect", [
     # the reference's grid (y half-widths up to 212): table LDS-staged 64-column tiles (ypass_t64), epochs of 4;
     # packed the row-pair y-pass in heaviest-first groups of 4; both with the y-pass ahead on its own stream
-    (dict(), "table", dict(rows_per_wave=1, ylds=3, yt_rows=1, yt_chunk=16, handoff_batch=4, ycoop=0, ypass_ahead=1)),
+    (dict(), "table", dict(rows_per_wave=1, ylds=3, yt_rows=2, yt_chunk=16, handoff_batch=4, ycoop=0, ypass_ahead=1)),
     (dict(), "packed", dict(rows_per_wave=1, ycoop=7, ycoop_order=4, ycoop_split=96, ycoop_split4=192, ylds=0,
                             handoff_batch=4, ypass_ahead=1)),
     # c3 (half-widths 4-64): table 4 rows per wave (ypass_table_kernel), no LDS staging, two generations per
@@ -357,7 +357,8 @@ def test_round5_tuning_keys_validate_on_host_only_handles():
     # the keys added in round 5 (t64 shapes, row-pair halves/quarters, y-pass ahead, ghost columns) are checked
     # and read back without a device: a host-only handle creates no stream and launches nothing
     f = host(coeff_mode="table")  # the reference's grid, row-uniform N: ypass_t64 by default
-    assert (f.get_tuning("yt_rows"), f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (1, 16, 2)
+    assert (f.get_tuning("yt_rows"), f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (2, 16, 2)
+    f.set_tuning("yt_rows", 1)
     f.set_tuning("yt_chunk", 24)
     assert (f.get_tuning("yt_chunk"), f.get_tuning("yt_pd")) == (24, 2)
     with pytest.raises(dfamd.DFError, match="yt_pd 4"):

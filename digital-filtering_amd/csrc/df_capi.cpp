@@ -2713,7 +2713,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
     else if (k == "zstage") h->zstage = value ? 2 : 0; // 0: the unstaged table z-pass that large halos take (tests)
     else if (k == "fused_exchange") h->fused_x = value != 0; // from the next df_filter on; the same on every rank
     else if (k == "ylds") { // LDS-staged table y-pass (2: ypass_tlds; 3: ypass_t64, 64-column tiles; 0: off)
-        if (value == 3 && !h->ylist) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
+        // (host-only handles have no list; the plane decides, as alloc_components does)
+        const bool t64_plane = h->device >= 0 ? h->ylist != nullptr
+                                              : h->coeff_mode == DF_COEFF_TABLE && !h->setup.per_cell;
+        if (value == 3 && !t64_plane) return fail(DF_EINVAL, "ylds 3 needs a table-mode plane with row-uniform N");
         if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {

@@ -194,7 +194,7 @@ def test_golden_native_grid(mode, tuning):
                                          ("table", dict(ylds=3, rows_per_wave=4)), ("table", dict(ylds=3)),
                                          ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
                                          ("table", dict(ylds=3, yt_rows=1, yt_pd=4)), ("table", dict(ylds=3, yt_rows=2, yt_chunk=8)),
-                                         ("table", dict(ylds=3, yt_chunk=24)),
+                                         ("table", dict(ylds=3, yt_rows=1, yt_chunk=24)),
                                          ("table", dict(ylds=3, yt_cl=1)), ("table", dict(ylds=3, yt_cl=1, yt_rows=1)),
                                          ("table", dict(ylds=3, yt_cl=1, yt_rows=4)),
                                          ("table", dict(ylds=3, yt_cl=1, yt_chunk=32)),

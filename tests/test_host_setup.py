@@ -388,3 +388,32 @@ def test_round5_tuning_keys_validate_on_host_only_handles():
     for v in (1, 0, 1):
         t.set_tuning("halo_ghost", v)
         assert t.get_tuning("halo_ghost") == v
+
+
+def _parametrized(src, func, arg):
+    i = src.index(f"def {func}")
+    j = src.rindex(f'@pytest.mark.parametrize("{arg}", ', 0, i)
+    blk = src[j + len(f'@pytest.mark.parametrize("{arg}", '):i].strip()
+    return eval(blk[:-1], {"dict": dict})  # the test file's own literal list
+
+
+def test_gpu_parity_tuning_sequences_are_accepted():
+    # every df_set_tuning sequence the GPU parity tests apply is valid for the plane it is applied to (checked here
+    # on host-only handles: a refused key would otherwise surface only on the GPU box, after minutes of queueing)
+    src = open(os.path.join(os.path.dirname(__file__), "test_gpu_parity.py")).read()
+    for mode, tuning in _parametrized(src, "test_native_grid_bitexact_vs_oracle", "mode,tuning"):
+        f = host(coeff_mode=mode)
+        for k, v in tuning.items():
+            f.set_tuning(k, v)
+    i = src.index("def test_runtime_tuning_is_bitexact")
+    a = src.index("settings = [", i)
+    b = src.index("]\n", a)
+    a2 = src.index("settings += [", b)
+    b2 = src.index("]\n", a2)
+    base = eval(src[a + len("settings = "):b + 1], {"dict": dict})
+    extra = eval(src[a2 + len("settings += "):b2 + 1], {"dict": dict})
+    for mode in ("packed", "table"):
+        f = host(plane="synthetic", Ny=131, Nz=260, N_min=2, N_max=16, coeff_mode=mode)
+        for kw in base + (extra if mode == "table" else []):
+            for k, v in kw.items():
+                f.set_tuning(k, v)

@@ -1289,7 +1289,8 @@ int build_ylists(df_handle *h)
 // The ypass_t64 shapes built (launch_ypass_t): scalar coefficient windows (cl 0) or LDS-staged ones (cl 1)
 bool t64_shape_ok(int cl, int R, int C, int PD)
 {
-    if (cl) return PD == 2 && ((R == 1 && C == 16) || (R == 2 && (C == 16 || C == 32)) || (R == 4 && C == 16));
+    if (cl) return (PD == 2 && ((R == 1 && C == 16) || (R == 2 && (C == 16 || C == 32)) || (R == 4 && C == 16))) ||
+                   (PD == 3 && C == 16 && (R == 1 || R == 2));
     if (PD == 4) return R == 1 && C == 16;
     return PD == 2 && ((R == 1 && (C == 16 || C == 24)) || (R == 2 && (C == 8 || C == 16)));
 }
@@ -2723,9 +2724,10 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {
-        if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
+        if (value < 2 || value > 4) return fail(DF_EINVAL, "yt_pd must be 2, 3 (yt_cl 1) or 4 (yt_cl 0)");
         if (!t64_shape_ok(h->yt_cl, h->yt_rows, h->yt_chunk, value))
-            return fail(DF_EINVAL, "yt_pd 4 is built for yt_rows 1 x yt_chunk 16 only (yt_cl 0)");
+            return fail(DF_EINVAL, "yt_pd " + std::to_string(value) + " is built for yt_rows 1 x yt_chunk 16 only (yt_cl 0: "
+                                   "prefetch 4; yt_cl 1: prefetch 3, rows 1 or 2)");
         h->yt_pd = value;
     } else if (k == "yt_cl") { // ypass_t64 coefficient staging: 1 LDS (shapes 1 x 16, 2 x 16, 2 x 32, 4 x 16), 0 SGPRs
         if (value != 0 && value != 1) return fail(DF_EINVAL, "yt_cl must be 0 or 1");

@@ -2055,12 +2055,15 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64l_kernel(SweepArgs a)
     bool on = live(0);
     __syncthreads();
     // whole groups of PD steps, as ypass_t64_kernel: steps past the last chunk stage and sum nothing; loads reach at
-    // most 2 PD C - 1 rows past the block's last (< kYTailRows) and coefficient windows read guard zeros
+    // most 2 PD C - 1 rows past the block's last (< kYTailRows) and coefficient windows read guard zeros.
+    // Chunk i + 1 is staged BEFORE chunk i is summed (the other LDS buffer, last read by chunk i - 1 before the
+    // previous barrier), so the barrier follows the sums directly: a long chain waits per chunk for the barrier
+    // alone, not for a store and its waits after its last add.
     auto step = [&](auto K, int i) {
         constexpr int k = decltype(K)::value;
         gload(K);
-        compute(i & 1, on);
         lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
+        compute(i & 1, on);
         on = live(i + 1);
         __syncthreads();
     };
@@ -2090,6 +2093,8 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
                 switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
                 case 1162: hipLaunchKernelGGL((ypass_t64l_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
                 case 2162: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
+                case 2163: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 16, 3>), grid, dim3(256), 0, st, a); break;
+                case 1163: hipLaunchKernelGGL((ypass_t64l_kernel<1, 4, 16, 3>), grid, dim3(256), 0, st, a); break;
                 case 2322: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 32, 2>), grid, dim3(256), 0, st, a); break;
                 case 4162: hipLaunchKernelGGL((ypass_t64l_kernel<4, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
                 default: return hipErrorInvalidValue; // df_set_tuning admits the shapes above only

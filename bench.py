@@ -744,6 +744,16 @@ def main(argv=None):
     f, rec = run_config(dfamd, ctx, wl, args, comm_id)
     recs = ctx.gather(rec)
     head = summarize(ctx, wl, args, recs)
+    # the headline handle's parity, then close it: the other mode's line below is timed without it resident beside
+    # (an idle handle's streams still take hardware queues)
+    parity = None
+    if args.parity == "on":
+        pr = parity_check(dfamd, ctx, wl, args, f, f.calls_done)
+        prs = ctx.gather(pr)
+        parity = {"ok": all(p["ok"] for p in prs), "reference": "whole plane, one GPU, table mode, same seed/calls",
+                  "calls_compared": f.calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
+    comm = f.comm_info() if ctx.world > 1 else None
+    f.close()
 
     alt = None
     if ctx.world > 1 and args.alt_modes == "auto":
@@ -814,14 +824,6 @@ def main(argv=None):
                                 "against tools/valu_probe's FP64 issue ceiling"}
         g.close()
 
-    parity = None
-    if args.parity == "on":
-        pr = parity_check(dfamd, ctx, wl, args, f, f.calls_done)
-        prs = ctx.gather(pr)
-        parity = {"ok": all(p["ok"] for p in prs), "reference": "whole plane, one GPU, table mode, same seed/calls",
-                  "calls_compared": f.calls_done, "ranks": prs if ctx.world > 1 else prs[0]}
-    comm = f.comm_info() if ctx.world > 1 else None
-    f.close()
     ctx.barrier()
     same = None
     if ctx.world > 1 and args.same_plane == "auto":

@@ -218,7 +218,6 @@ struct df_handle {
     int cur = 0;                // noise set of the current step
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
     int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
-    int yt_cl = 0; // ypass_t64: 1 = the chunk coefficients staged in LDS (ypass_t64l_kernel), 0 = scalar windows
     int yt_limit = 0; // timing only (DFAMD_YT_LIMIT): ypass_t64 launches the first yt_limit blocks of its list alone
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
@@ -404,7 +403,6 @@ SweepArgs sweep_args(df_handle *h)
     a.ylist_ncol = h->ylist_ncol;
     a.ylist_R = h->yt_rows;
     a.ylist_C = h->yt_chunk;
-    a.ylist_cl = h->yt_cl;
     a.ylist_PD = h->yt_pd;
     for (int c = 0; c < 3; ++c) {
         a.yout[c] = h->c[c].Nzp;
@@ -1286,11 +1284,9 @@ int build_ylists(df_handle *h)
     return rc;
 }
 
-// The ypass_t64 shapes built (launch_ypass_t): scalar coefficient windows (cl 0) or LDS-staged ones (cl 1)
-bool t64_shape_ok(int cl, int R, int C, int PD)
+// The ypass_t64 shapes built (launch_ypass_t)
+bool t64_shape_ok(int R, int C, int PD)
 {
-    if (cl) return (PD == 2 && ((R == 1 && C == 16) || (R == 2 && (C == 16 || C == 32)) || (R == 4 && C == 16))) ||
-                   (PD == 3 && C == 16 && (R == 1 || R == 2));
     if (PD == 4) return R == 1 && C == 16;
     return PD == 2 && ((R == 1 && (C == 16 || C == 24)) || (R == 2 && (C == 8 || C == 16)));
 }
@@ -2680,7 +2676,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
     const std::string k(key);
     const std::pair<const char *, int> keys[] = {
         {"rows_per_wave", h->rows_per_wave}, {"yunroll", h->yunroll}, {"ycoop", h->ycoop},
-        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"yt_cl", h->yt_cl}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
+        {"ycoop_order", h->ycoop_order}, {"ycoop_split", h->ycoop_split}, {"ycoop_split4", h->ycoop_split4}, {"ylds", h->ylds}, {"yt_rows", h->yt_rows}, {"yt_chunk", h->yt_chunk}, {"yt_pd", h->yt_pd}, {"zsplit", h->zsplit}, {"ypass_ahead", h->yahead},
         {"zstage", h->zstage}, {"nt_stores", h->nt_stores}, {"ywin_T", h->ywin_T}, {"ywin_W", h->ywin_W}, {"zwin_T", h->zwin_T},
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
@@ -2724,23 +2720,14 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         if (value == 3 && !t64_fits(h)) return fail(DF_EINVAL, "ylds 3 needs r_ys under 4 GiB per component");
         h->ylds = value == 3 ? 3 : value ? 2 : 0;
     } else if (k == "yt_pd") {
-        if (value < 2 || value > 4) return fail(DF_EINVAL, "yt_pd must be 2, 3 (yt_cl 1) or 4 (yt_cl 0)");
-        if (!t64_shape_ok(h->yt_cl, h->yt_rows, h->yt_chunk, value))
-            return fail(DF_EINVAL, "yt_pd " + std::to_string(value) + " is built for yt_rows 1 x yt_chunk 16 only (yt_cl 0: "
-                                   "prefetch 4; yt_cl 1: prefetch 3, rows 1 or 2)");
+        if (value != 2 && value != 4) return fail(DF_EINVAL, "yt_pd must be 2 or 4");
+        if (!t64_shape_ok(h->yt_rows, h->yt_chunk, value))
+            return fail(DF_EINVAL, "yt_pd 4 is built for yt_rows 1 x yt_chunk 16 only");
         h->yt_pd = value;
-    } else if (k == "yt_cl") { // ypass_t64 coefficient staging: 1 LDS (shapes 1 x 16, 2 x 16, 2 x 32, 4 x 16), 0 SGPRs
-        if (value != 0 && value != 1) return fail(DF_EINVAL, "yt_cl must be 0 or 1");
-        if (!t64_shape_ok(value, h->yt_rows, h->yt_chunk, h->yt_pd))
-            return fail(DF_EINVAL, "yt_cl " + std::to_string(value) + " has no " + std::to_string(h->yt_rows) + " x " +
-                                       std::to_string(h->yt_chunk) + " (prefetch " + std::to_string(h->yt_pd) + ") shape");
-        h->yt_cl = value;
     } else if (k == "yt_rows" || k == "yt_chunk") { // ypass_t64 shapes (rows x chunk), t64_shape_ok
         const int R = k == "yt_rows" ? value : h->yt_rows, C = k == "yt_chunk" ? value : h->yt_chunk;
-        const int Cu = k == "yt_rows" && !t64_shape_ok(h->yt_cl, R, C, 2) ? 16 : C; // a row count alone: chunks of 16
-        if (!t64_shape_ok(h->yt_cl, R, Cu, 2))
-            return fail(DF_EINVAL, h->yt_cl ? "yt_rows x yt_chunk must be 1 x 16, 2 x 16, 2 x 32 or 4 x 16 (yt_cl 1)"
-                                            : "yt_rows x yt_chunk must be 1 x 16, 1 x 24, 2 x 8 or 2 x 16");
+        const int Cu = k == "yt_rows" && !t64_shape_ok(R, C, 2) ? 16 : C; // a row count alone: chunks of 16
+        if (!t64_shape_ok(R, Cu, 2)) return fail(DF_EINVAL, "yt_rows x yt_chunk must be 1 x 16, 1 x 24, 2 x 8 or 2 x 16");
         if (h->device >= 0)
             if (int rc = sync_all(h)) return rc; // a queued y-pass may still read the old order
         h->yt_rows = R;

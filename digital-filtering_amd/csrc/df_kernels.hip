@@ -1943,141 +1943,6 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     }
 }
 
-// ypass_t64 with the coefficients staged in LDS (SweepArgs::ylist_cl, round 6). The scalar-window form exposes one
-// scalar load per chunk: it can only be waited for with the LDS reads (one lgkm counter, scalar loads returning
-// out of order), so it is issued just before the chunk's barrier and its latency lands on every chunk of the
-// longest blocks' serial chains - the kernel's critical path. Here each chunk's R x C coefficients (the same
-// zero-guarded windows) travel like its noise: a vector load PD chunks ahead (lanes r C + q of wave w load tap q of
-// row r's window; a row with no tap in the chunk loads the table's leading zeros), a store to LDS beside the noise,
-// and broadcast ds_read_b128 pairs in the sums. No scalar memory in the loop, every LDS wait counted, and the
-// scalar registers no longer cap R x C. Same products in the same order: bit-identical to ypass_t64_kernel.
-template <int R, int NW, int C, int PD>
-__global__ __launch_bounds__(64 * NW) void ypass_t64l_kernel(SweepArgs a)
-{
-    constexpr int LP = C / (2 * NW); // pairs of chunk rows each wave loads
-    static_assert(C % (2 * NW) == 0, "chunk row pairs split evenly over the waves");
-    static_assert(R * C <= 64, "a wave loads its rows' windows one tap per lane");
-    __shared__ dvec2 nbuf[2][C / 2][64];
-    __shared__ dvec2 cbuf[2][NW][R * C / 2]; // wave w, row r: taps 2p, 2p + 1 at [r C / 2 + p]
-    const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
-    const int tile = a.ylist[blockIdx.x];
-    const int nrb = a.ylist_nrb, ncol = a.ylist_ncol;
-    const int rb = tile % nrb, ct = (tile / nrb) % ncol, c = tile / (nrb * ncol);
-    if (!((a.comps_mask >> c) & 1)) return; // block-uniform
-    const int Ny = a.Ny, RB = NW * R, j0 = rb * RB;
-    const int *nst = a.Ny_st[c] + (size_t)(ct >> 1) * Ny;
-    int mlo = 1 << 30, mhi = -(1 << 30);
-    for (int q = 0; q < RB && j0 + q < Ny; ++q) {
-        const int N = nst[j0 + q];
-        mlo = min(mlo, j0 + q - N);
-        mhi = max(mhi, j0 + q + N);
-    }
-    const int jw = j0 + w * R;
-    int ilo[R];
-    unsigned iw[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        ilo[r] = 1 << 30;
-        iw[r] = 0;
-        if (jw + r < Ny) {
-            const int N = nst[jw + r], lo = jw + r - N;
-            ilo[r] = (lo - mlo) / C;
-            iw[r] = (unsigned)((jw + r + N - mlo) / C - ilo[r]);
-        }
-    }
-    // this lane's coefficient load: tap lq of row lr's window (lanes past R C idle); its window moves C taps a chunk
-    const int lr = lane / C, lq = lane - lr * C;
-    const bool cl_lane = lane < R * C;
-    int lr_ilo = 1 << 30;
-    unsigned lr_iw = 0;
-    const double *lwin = a.tabf;
-    if (cl_lane && jw + lr < Ny) {
-        const int N = nst[jw + lr], lo = jw + lr - N;
-        lr_ilo = (lo - mlo) / C;
-        lr_iw = (unsigned)((jw + lr + N - mlo) / C - lr_ilo);
-        lwin = a.tabf + a.tabf_off[N] + (mlo - lo) + lq;
-    }
-    const int col = ct * 64 + lane;
-    const unsigned Pz8 = (unsigned)a.Pz * 8u;
-    const char *nb = reinterpret_cast<const char *>(a.ry[c]), *nb1 = nb + Pz8;
-    unsigned vo[LP];
-#pragma unroll
-    for (int k = 0; k < LP; ++k) vo[k] = (unsigned)(a.Nyp[c] + mlo + 2 * (w + NW * k)) * Pz8 + (unsigned)col * 8u;
-    dvec2 pre[PD][LP];
-    double cpre[PD];
-    int gi = 0; // the chunk the next gload fetches
-    auto gload = [&](auto K) {
-        constexpr int k0 = decltype(K)::value;
-#pragma unroll
-        for (int k = 0; k < LP; ++k) {
-            pre[k0][k] = dvec2{*reinterpret_cast<const double *>(nb + vo[k]),
-                               *reinterpret_cast<const double *>(nb1 + vo[k])};
-            vo[k] += (unsigned)C * Pz8;
-        }
-        if (cl_lane) {
-            const bool lv = (unsigned)(gi - lr_ilo) <= lr_iw;
-            cpre[k0] = lv ? lwin[gi * C] : a.tabf[lq]; // a.tabf: kTabGuard leading zeros
-        }
-        ++gi;
-    };
-    auto lstore = [&](auto K, int buf) {
-        constexpr int k0 = decltype(K)::value;
-#pragma unroll
-        for (int k = 0; k < LP; ++k) nbuf[buf][w + NW * k][lane] = pre[k0][k];
-        if (cl_lane) reinterpret_cast<double *>(cbuf[buf][w])[lane] = cpre[k0];
-    };
-    auto live = [&](int i) {
-        bool f = false;
-#pragma unroll
-        for (int r = 0; r < R; ++r) f = f || (unsigned)(i - ilo[r]) <= iw[r];
-        return f;
-    };
-    double acc[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.0;
-    auto compute = [&](int buf, bool on) {
-        if (!on) return;
-#pragma unroll
-        for (int p = 0; p < C / 2; ++p) {
-            const dvec2 n = nbuf[buf][p][lane];
-            dvec2 b[R];
-#pragma unroll
-            for (int r = 0; r < R; ++r) b[r] = cbuf[buf][w][r * (C / 2) + p];
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += b[r].x * n.x;
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += b[r].y * n.y;
-        }
-    };
-    const int nch = (mhi - mlo) / C + 1;
-    unroll_to<0, PD>([&](auto K) { gload(K); });
-    lstore(ic_t<0>{}, 0);
-    bool on = live(0);
-    __syncthreads();
-    // whole groups of PD steps, as ypass_t64_kernel: steps past the last chunk stage and sum nothing; loads reach at
-    // most 2 PD C - 1 rows past the block's last (< kYTailRows) and coefficient windows read guard zeros.
-    // Chunk i + 1 is staged BEFORE chunk i is summed (the other LDS buffer, last read by chunk i - 1 before the
-    // previous barrier), so the barrier follows the sums directly: a long chain waits per chunk for the barrier
-    // alone, not for a store and its waits after its last add.
-    auto step = [&](auto K, int i) {
-        constexpr int k = decltype(K)::value;
-        gload(K);
-        lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
-        compute(i & 1, on);
-        on = live(i + 1);
-        __syncthreads();
-    };
-    for (int i = 0; i < nch; i += PD) unroll_to<0, PD>([&](auto K) { step(K, i + decltype(K)::value); });
-    if (col < a.ylo[c] || col >= a.yhi[c]) return;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (jw + r >= Ny) continue;
-        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.yout[c] + col;
-        if (a.ynt_stores) __builtin_nontemporal_store(acc[r], o);
-        else *o = acc[r];
-    }
-}
-
 template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
 {
     if constexpr (TABLE) {
@@ -2089,18 +1954,6 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
             // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 1 x 24 26.6 (the call beside the
             // RNG -2%, profiles/r5/p), 2 x 16 26.6, 2 x 8 35-39, the round-4 ypass_tlds 40.4; 4 chunks in flight lose
             // (VGPRs 38 -> 114) except on a lone block
-            if (a.ylist_cl) { // coefficients staged in LDS (ypass_t64l_kernel)
-                switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
-                case 1162: hipLaunchKernelGGL((ypass_t64l_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-                case 2162: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-                case 2163: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 16, 3>), grid, dim3(256), 0, st, a); break;
-                case 1163: hipLaunchKernelGGL((ypass_t64l_kernel<1, 4, 16, 3>), grid, dim3(256), 0, st, a); break;
-                case 2322: hipLaunchKernelGGL((ypass_t64l_kernel<2, 4, 32, 2>), grid, dim3(256), 0, st, a); break;
-                case 4162: hipLaunchKernelGGL((ypass_t64l_kernel<4, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
-                default: return hipErrorInvalidValue; // df_set_tuning admits the shapes above only
-                }
-                return hipGetLastError();
-            }
             switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
             case 1162: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
             case 1164: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 4>), grid, dim3(256), 0, st, a); break;

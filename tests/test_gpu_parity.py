@@ -195,9 +195,6 @@ def test_golden_native_grid(mode, tuning):
                                          ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
                                          ("table", dict(ylds=3, yt_rows=1, yt_pd=4)), ("table", dict(ylds=3, yt_rows=2, yt_chunk=8)),
                                          ("table", dict(ylds=3, yt_rows=1, yt_chunk=24)),
-                                         ("table", dict(ylds=3, yt_cl=1)), ("table", dict(ylds=3, yt_cl=1, yt_rows=1)),
-                                         ("table", dict(ylds=3, yt_cl=1, yt_rows=4)),
-                                         ("table", dict(ylds=3, yt_cl=1, yt_chunk=32)),
                                          ("table", dict(ylds=0))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
@@ -330,8 +327,7 @@ def test_runtime_tuning_is_bitexact(mode):
     if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back
         settings += [dict(ylds=3, yt_rows=1), dict(yt_rows=2), dict(yt_chunk=8), dict(yt_rows=1, yt_pd=4), dict(yt_pd=2),
                      dict(yt_chunk=24),
-                     dict(yt_rows=2, yt_chunk=16), dict(yt_cl=1), dict(yt_rows=4), dict(yt_rows=2, yt_chunk=32),
-                     dict(yt_rows=1), dict(yt_rows=2, yt_cl=0), dict(ylds=2), dict(ylds=0)]
+                     dict(yt_rows=2, yt_chunk=16), dict(ylds=2), dict(ylds=0)]
     for kw in settings:
         for k, v in kw.items():
             b.set_tuning(k, v)

@@ -1484,9 +1484,13 @@ int plan_rng(df_handle *h)
     }
     // K3 splits each attempt wave over up to 16 waves while the plane has fewer than ~4 waves of
     // attempts per SIMD (c1: 140 waves; the reference's grid: ~750): a wave's 16 serial polar
-    // iterations (log, sqrt, divide in FP64) otherwise set K3's time on small planes.
+    // iterations (log, sqrt, divide in FP64) otherwise set K3's time on small planes. Packed planes aim at
+    // half of that (round 6): their K3 runs beside HBM-bound sweeps, whose bandwidth its extra waves take
+    // (c2 packed -4..-5% per call with gen_split 2 against 4, both orders; c1, the reference's grid and the
+    // table planes neutral; profiles/r6/k)
+    const long long k3_waves = h->coeff_mode == DF_COEFF_PACKED ? 2048 : 4096;
     g.gen_split = 1;
-    while (g.gen_split < kRngPerThread && (long long)h->rng_blocks * kWavesPerBlock * g.gen_split < 4096)
+    while (g.gen_split < kRngPerThread && (long long)h->rng_blocks * kWavesPerBlock * g.gen_split < k3_waves)
         g.gen_split *= 2;
     if (g.gen_split < 1 || g.gen_split > kRngPerThread || (g.gen_split & (g.gen_split - 1)))
         return fail(DF_EINVAL, "gen_split must be a power of two <= 16");

@@ -340,7 +340,9 @@ def test_alloc_registry_rejects_overlapping_ranges():
      dict(rows_per_wave=2, ylds=0, ycoop=0, handoff_batch=1, ypass_ahead=0)),
     # c2: epochs of 2; packed: a wave per component in the z-pass
     (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(rows_per_wave=4, ylds=0, handoff_batch=2)),
-    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "packed", dict(rows_per_wave=2, zsplit=1, handoff_batch=2)),
+    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "packed",
+     dict(rows_per_wave=2, zsplit=1, handoff_batch=2, gen_split=2)),
+    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(gen_split=4)),
     (dict(), "packed", dict(zsplit=0)),
 ])
 def test_launch_plan_defaults(plane, mode, expect):

@@ -49,6 +49,16 @@ module df_c_binding
         type(c_ptr) :: grid_y, grid_z
     end type df_config_c
 
+    ! struct df_profile and struct df_comm_stats (df_c.h)
+    type, bind(C) :: df_profile
+        integer(c_long_long) :: calls
+        real(c_double) :: rng_ms, ypass_ms, halo_ms, zpass_ms, total_ms
+    end type df_profile
+    type, bind(C) :: df_comm_stats
+        integer(c_int) :: rccl_ranks, rccl_rank, halo_peers, rng_collective
+        integer(c_long_long) :: halo_bytes_sent, rng_bytes_received, rng_blocks_counted, rng_blocks_total
+    end type df_comm_stats
+
     interface
         subroutine df_config_default(cfg) bind(C, name="df_config_default")
             import :: df_config_c
@@ -170,6 +180,157 @@ module df_c_binding
         end function
         integer(c_int) function df_abi_version() bind(C, name="df_abi_version")
             import :: c_int
+        end function
+        ! ---- the rest of df_c.h: strip groups, the stage API, setup queries, tuning, profiling, diagnostics
+        type(c_ptr) function df_data_dir() bind(C, name="df_data_dir")
+            import :: c_ptr
+        end function
+        integer(c_int) function df_create_group(cfgs, n, out) bind(C, name="df_create_group")
+            import :: c_int, c_ptr, df_config_c
+            type(df_config_c), intent(in) :: cfgs(*)
+            integer(c_int), value :: n
+            type(c_ptr), intent(out) :: out(*)
+        end function
+        integer(c_int) function df_filter_group(hs, n, dt) bind(C, name="df_filter_group")
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), intent(in) :: hs(*)
+            integer(c_int), value :: n
+            real(c_double), value :: dt
+        end function
+        integer(c_int) function df_generate_white_noise(h) bind(C, name="df_generate_white_noise")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+        end function
+        integer(c_int) function df_filtering_sweeps(h, comp) bind(C, name="df_filtering_sweeps")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp
+        end function
+        integer(c_int) function df_correlate_fields(h, comp, dt) bind(C, name="df_correlate_fields")
+            import :: c_ptr, c_int, c_double
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp
+            real(c_double), value :: dt
+        end function
+        integer(c_int) function df_apply_RST_scaling(h) bind(C, name="df_apply_RST_scaling")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+        end function
+        integer(c_int) function df_get_rho_T_fluc(h) bind(C, name="df_get_rho_T_fluc")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+        end function
+        integer(c_int) function df_alloc_registry(p, bytes, claim) bind(C, name="df_alloc_registry")
+            import :: c_ptr, c_size_t, c_int
+            type(c_ptr), value :: p
+            integer(c_size_t), value :: bytes
+            integer(c_int), value :: claim
+        end function
+        integer(c_long_long) function df_alloc_registry_count() bind(C, name="df_alloc_registry_count")
+            import :: c_long_long
+        end function
+        integer(c_int) function df_set_field(h, which, host_in) bind(C, name="df_set_field")
+            import :: c_ptr, c_int, c_double
+            type(c_ptr), value :: h
+            integer(c_int), value :: which
+            real(c_double), intent(in) :: host_in(*)
+        end function
+        integer(c_int) function df_get_offsets(h, comp, dir, out) bind(C, name="df_get_offsets")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp, dir
+            integer(c_int), intent(out) :: out(*)
+        end function
+        integer(c_int) function df_get_comp_info(h, comp, Ny_max, Nz_max, by_size, bz_size) &
+                bind(C, name="df_get_comp_info")
+            import :: c_ptr, c_int, c_long_long
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp
+            integer(c_int), intent(out) :: Ny_max, Nz_max
+            integer(c_long_long), intent(out) :: by_size, bz_size
+        end function
+        integer(c_int) function df_get_coeffs(h, comp, dir, out, n) bind(C, name="df_get_coeffs")
+            import :: c_ptr, c_int, c_double, c_long_long
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp, dir
+            real(c_double), intent(out) :: out(*)
+            integer(c_long_long), value :: n
+        end function
+        integer(c_int) function df_set_rng_state(h, state, saved_flag, saved) bind(C, name="df_set_rng_state")
+            import :: c_ptr, c_int, c_int64_t, c_double
+            type(c_ptr), value :: h
+            integer(c_int64_t), value :: state
+            integer(c_int), value :: saved_flag
+            real(c_double), value :: saved
+        end function
+        integer(c_int) function df_get_noise(h, comp, dir, out, n) bind(C, name="df_get_noise")
+            import :: c_ptr, c_int, c_double, c_long_long
+            type(c_ptr), value :: h
+            integer(c_int), value :: comp, dir
+            real(c_double), intent(out) :: out(*)
+            integer(c_long_long), value :: n
+        end function
+        integer(c_long_long) function df_rms_count(h) bind(C, name="df_rms_count")
+            import :: c_ptr, c_long_long
+            type(c_ptr), value :: h
+        end function
+        integer(c_int) function df_get_vertices(h, y, z) bind(C, name="df_get_vertices")
+            import :: c_ptr, c_int, c_double
+            type(c_ptr), value :: h
+            real(c_double), intent(out) :: y(*), z(*)
+        end function
+        integer(c_int) function df_get_grid(h, y, z) bind(C, name="df_get_grid")
+            import :: c_ptr, c_int, c_double
+            type(c_ptr), value :: h
+            real(c_double), intent(out) :: y(*), z(*)
+        end function
+        integer(c_int) function df_plane_info(h, plane, per_cell) bind(C, name="df_plane_info")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+            integer(c_int), intent(out) :: plane, per_cell
+        end function
+        integer(c_int) function df_set_tuning(h, key, value) bind(C, name="df_set_tuning")
+            import :: c_ptr, c_int, c_char
+            type(c_ptr), value :: h
+            character(kind=c_char), intent(in) :: key(*) ! NUL-terminated: trim(k) // c_null_char
+            integer(c_int), value :: value
+        end function
+        integer(c_int) function df_get_tuning(h, key, value) bind(C, name="df_get_tuning")
+            import :: c_ptr, c_int, c_char
+            type(c_ptr), value :: h
+            character(kind=c_char), intent(in) :: key(*)
+            integer(c_int), intent(out) :: value
+        end function
+        integer(c_int) function df_set_profiling(h, on) bind(C, name="df_set_profiling")
+            import :: c_ptr, c_int
+            type(c_ptr), value :: h
+            integer(c_int), value :: on
+        end function
+        integer(c_int) function df_get_profile(h, out) bind(C, name="df_get_profile")
+            import :: c_ptr, c_int, df_profile
+            type(c_ptr), value :: h
+            type(df_profile), intent(out) :: out
+        end function
+        real(c_double) function df_algorithmic_bytes(h, kernel) bind(C, name="df_algorithmic_bytes")
+            import :: c_ptr, c_int, c_double
+            type(c_ptr), value :: h
+            integer(c_int), value :: kernel
+        end function
+        integer(c_int) function df_comm_unique_id(out, len) bind(C, name="df_comm_unique_id")
+            import :: c_ptr, c_size_t, c_int
+            type(c_ptr), value :: out
+            integer(c_size_t), value :: len
+        end function
+        integer(c_int) function df_comm_info(h, out) bind(C, name="df_comm_info")
+            import :: c_ptr, c_int, df_comm_stats
+            type(c_ptr), value :: h
+            type(df_comm_stats), intent(out) :: out
+        end function
+        integer(c_long_long) function df_trace(h, out, cap) bind(C, name="df_trace")
+            import :: c_ptr, c_long_long
+            type(c_ptr), value :: h
+            integer(c_long_long), intent(out) :: out(*)
+            integer(c_long_long), value :: cap
         end function
     end interface
 

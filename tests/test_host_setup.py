@@ -419,3 +419,11 @@ def test_gpu_parity_tuning_sequences_are_accepted():
         for kw in base + (extra if mode == "table" else []):
             for k, v in kw.items():
                 f.set_tuning(k, v)
+
+
+def test_fortran_module_binds_every_c_entry_point():
+    # include/digital_filtering.f90's df_c_binding: one bind(C) interface per function df_c.h declares
+    import re
+    f90 = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "digital_filtering.f90")).read()
+    bound = set(re.findall(r'bind\(C, name="(df_\w+)"\)', f90))
+    assert [s for s in dfamd.header_symbols() if s not in bound] == []

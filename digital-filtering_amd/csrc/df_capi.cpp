@@ -219,6 +219,7 @@ struct df_handle {
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
     int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
     int yt_limit = 0; // timing only (DFAMD_YT_LIMIT): ypass_t64 launches the first yt_limit blocks of its list alone
+    int yt_dbg = 0;   // timing only (DFAMD_YT_DEBUG, wrong sums): ypass_t64 ablations of its coefficient loads
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
@@ -399,6 +400,7 @@ SweepArgs sweep_args(df_handle *h)
     a.ylds = h->ylds;
     a.ylist = h->ylist;
     a.ylist_n = h->yt_limit > 0 ? std::min(h->ylist_n, h->yt_limit) : h->ylist_n;
+    a.ylist_dbg = h->yt_dbg;
     a.ylist_nrb = h->ylist_nrb;
     a.ylist_ncol = h->ylist_ncol;
     a.ylist_R = h->yt_rows;
@@ -1157,6 +1159,7 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
     // timing ablation (wrong fields by design): ypass_t64 runs only the first n blocks of its heaviest-first list
     if (const char *e = std::getenv("DFAMD_YT_LIMIT")) h->yt_limit = std::atoi(e);
+    if (const char *e = std::getenv("DFAMD_YT_DEBUG")) h->yt_dbg = std::atoi(e);
     if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
         h->rows_per_wave != 8)
         return fail(DF_EINVAL, "rows_per_wave must be 1, 2, 4 or 8");

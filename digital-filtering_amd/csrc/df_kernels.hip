@@ -1811,7 +1811,9 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 // whether the row has a tap in the chunk is a compare of the chunk index against a range fixed at the start.
 // Each row adds its taps in the order i = -N..N (noise rows ascending) with df.cpp:373-375's products:
 // bit-identical to every other form.
-template <int R, int NW, int C, int PD>
+// DBG (timing ablations, wrong sums; DFAMD_YT_DEBUG): 1 no coefficient loads after chunk 0, 4 every row of a
+// wave sums with row 0's window
+template <int R, int NW, int C, int PD, int DBG = 0>
 __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 {
     constexpr int LP = C / (2 * NW); // pairs of chunk rows each wave loads
@@ -1889,7 +1891,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
     double cw[R][C]; // the chunk's coefficients (uniform), loaded whether or not the chunk is live (no branch)
     auto cload = [&](int i) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+        for (int r = 0; r < (DBG == 4 ? 1 : R); ++r) {
             const double *src = liv[r] ? cwin[r] + i * C : a.tabf; // a.tabf: kTabGuard zeros
 #pragma unroll
             for (int q = 0; q < C; ++q) cw[r][q] = src[q];
@@ -1904,9 +1906,9 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         for (int p = 0; p < C / 2; ++p) {
             const dvec2 n = nbuf[buf][p][lane];
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p] * n.x;
+            for (int r = 0; r < R; ++r) acc[r] += cw[DBG == 4 ? 0 : r][2 * p] * n.x;
 #pragma unroll
-            for (int r = 0; r < R; ++r) acc[r] += cw[r][2 * p + 1] * n.y;
+            for (int r = 0; r < R; ++r) acc[r] += cw[DBG == 4 ? 0 : r][2 * p + 1] * n.y;
         }
     };
     // chunk i: rows mlo + C i ..; its loads in register set i % PD, its sums from LDS buffer i % 2 (as
@@ -1929,7 +1931,7 @@ __global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
         compute(i & 1, on);
         lstore(ic_t<(k + 1) % PD>{}, (i + 1) & 1);
         on = live(i + 1);
-        cload(i + 1);
+        if constexpr (DBG != 1) cload(i + 1);
         __syncthreads();
     };
     for (int i = 0; i < nch; i += PD) unroll_to<0, PD>([&](auto K) { step(K, i + decltype(K)::value); });
@@ -1954,6 +1956,13 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
             // measured on the reference's grid (profiles/r5): 1 x 16 24.7-25.1 us, 1 x 24 26.6 (the call beside the
             // RNG -2%, profiles/r5/p), 2 x 16 26.6, 2 x 8 35-39, the round-4 ypass_tlds 40.4; 4 chunks in flight lose
             // (VGPRs 38 -> 114) except on a lone block
+            if (a.ylist_dbg && a.ylist_C == 16 && a.ylist_PD == 2) { // timing ablations (DFAMD_YT_DEBUG)
+                if (a.ylist_dbg == 1 && a.ylist_R == 1) hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2, 1>), grid, dim3(256), 0, st, a);
+                else if (a.ylist_dbg == 1 && a.ylist_R == 2) hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2, 1>), grid, dim3(256), 0, st, a);
+                else if (a.ylist_dbg == 4 && a.ylist_R == 2) hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2, 4>), grid, dim3(256), 0, st, a);
+                else return hipErrorInvalidValue;
+                return hipGetLastError();
+            }
             switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {
             case 1162: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 2>), grid, dim3(256), 0, st, a); break;
             case 1164: hipLaunchKernelGGL((ypass_t64_kernel<1, 4, 16, 4>), grid, dim3(256), 0, st, a); break;

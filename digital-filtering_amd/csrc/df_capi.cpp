@@ -219,11 +219,8 @@ struct df_handle {
     int ylds = 0; // table y-pass with LDS-staged noise (SweepArgs::ylds): 2 ypass_tlds, 3 ypass_t64
     int yt_rows = 1, yt_chunk = 16, yt_pd = 2; // ypass_t64: rows per wave, noise rows per LDS chunk, chunks in flight
     int yt_limit = 0; // timing only (DFAMD_YT_LIMIT): ypass_t64 launches the first yt_limit blocks of its list alone
-    int yt_skip = 0;  // timing only (DFAMD_YT_SKIP): ... or all but its first yt_skip blocks
     int yt_dbg = 0;   // timing only (DFAMD_YT_DEBUG, wrong sums): ypass_t64 ablations of its coefficient loads
     int *ylist = nullptr;    // ypass_t64 dispatch order (build_ylist)
-    int yt_mix = 0;          // ypass_t64 at 2 rows: its yt_mix heaviest blocks as 1-row blocks (ypass_t64_mix_kernel)
-    int ylist_nh = 0, ylist_nrb1 = 0; // ... their entries at the list's head, and 1-row blocks per column tile
     int ylist_n = 0, ylist_nrb = 0, ylist_ncol = 0, ylist_cap = 0;
     // Ghost columns (round 5, table-mode z-strips with row-uniform N): each rank y-filters its strip widened by
     // Gl / Gr columns of its neighbours' (the widest z half-width, Nzp), straight into its z-halo, so the z-pass
@@ -401,12 +398,9 @@ SweepArgs sweep_args(df_handle *h)
         a.ycoop2_perm[c] = h->ycoop_order || h->ycoop_split || h->ycoop_split4 ? h->c[c].ycoop2_perm : nullptr;
     }
     a.ylds = h->ylds;
-    a.ylist = h->ylist + std::max(0, std::min(h->yt_skip, h->ylist_n - 1));
-    a.ylist_n = std::max(1, (h->yt_limit > 0 ? std::min(h->ylist_n, h->yt_limit) : h->ylist_n) -
-                                std::min(h->yt_skip, h->ylist_n - 1));
+    a.ylist = h->ylist;
+    a.ylist_n = h->yt_limit > 0 ? std::min(h->ylist_n, h->yt_limit) : h->ylist_n;
     a.ylist_dbg = h->yt_dbg;
-    a.ylist_nh = h->ylist_nh;
-    a.ylist_nrb1 = h->ylist_nrb1;
     a.ylist_nrb = h->ylist_nrb;
     a.ylist_ncol = h->ylist_ncol;
     a.ylist_R = h->yt_rows;
@@ -905,7 +899,6 @@ int phase_ypass(df_handle *h, int comps_mask, int set, hipStream_t st, long long
         a.nstrips = h->nstrips_g;
         a.ylist = h->ylist_g;
         a.ylist_n = h->ylist_g_n;
-        a.ylist_nh = 0; // (the widened strip's list has no 1-row head)
         a.ylist_nrb = h->ylist_g_nrb;
         a.ylist_ncol = h->ylist_g_ncol;
         for (int c = 0; c < 3; ++c) {
@@ -1166,7 +1159,6 @@ int read_config(df_handle *h, const df_config_c *cfg)
     if (const char *e = std::getenv("DFAMD_RNG_DEBUG")) h->geom.debug_flags = std::atoi(e); // timing ablation
     // timing ablation (wrong fields by design): ypass_t64 runs only the first n blocks of its heaviest-first list
     if (const char *e = std::getenv("DFAMD_YT_LIMIT")) h->yt_limit = std::atoi(e);
-    if (const char *e = std::getenv("DFAMD_YT_SKIP")) h->yt_skip = std::max(0, std::atoi(e));
     if (const char *e = std::getenv("DFAMD_YT_DEBUG")) h->yt_dbg = std::atoi(e);
     if (h->rows_per_wave != 0 && h->rows_per_wave != 1 && h->rows_per_wave != 2 && h->rows_per_wave != 4 &&
         h->rows_per_wave != 8)
@@ -1282,27 +1274,10 @@ int build_ylist(df_handle *h, bool ghost)
     std::stable_sort(cost.begin(), cost.end(), [](const auto &p, const auto &q) { return p.first < q.first; });
     std::vector<int> order(n);
     for (int i = 0; i < n; ++i) order[i] = cost[i].second;
-    if (!ghost) { // yt_mix: the heaviest 2-row blocks split into their two 1-row halves, at the list's head
-        h->ylist_nh = 0;
-        const int nrb1 = (Ny + 3) / 4, k = h->yt_rows == 2 && h->yt_chunk == 16 && h->yt_pd == 2 ? std::min(h->yt_mix, n) : 0;
-        if (k > 0) {
-            std::vector<int> mix;
-            for (int i = 0; i < k; ++i) {
-                const int t = order[i], rb = t % nrb, cc = t / nrb; // cc = c * ncol + ct
-                for (int hb = 2 * rb; hb < std::min(2 * rb + 2, nrb1); ++hb) mix.push_back(cc * nrb1 + hb);
-            }
-            h->ylist_nh = (int)mix.size();
-            mix.insert(mix.end(), order.begin() + k, order.end());
-            if ((int)mix.size() > h->ylist_cap) return fail(DF_EINVAL, "ypass_t64 tile list larger than its allocation");
-            order.swap(mix);
-        }
-        h->ylist_nrb1 = nrb1;
-    }
-    const int nlist = (int)order.size();
-    (ghost ? h->ylist_g_n : h->ylist_n) = nlist;
+    (ghost ? h->ylist_g_n : h->ylist_n) = n;
     (ghost ? h->ylist_g_nrb : h->ylist_nrb) = nrb;
     (ghost ? h->ylist_g_ncol : h->ylist_ncol) = ncol;
-    return upload(h, ghost ? h->ylist_g : h->ylist, order.data(), (size_t)nlist);
+    return upload(h, ghost ? h->ylist_g : h->ylist, order.data(), order.size());
 }
 
 int build_ylists(df_handle *h)
@@ -2713,7 +2688,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
         {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap},
-        {"halo_ghost", h->ghost}, {"yt_mix", h->yt_mix},
+        {"halo_ghost", h->ghost},
         // read-only: noise sets allocated at create, epochs generated ahead of the one consumed (prefetch_epochs)
         {"noise_sets", h->nsets}, {"prefetch_epochs", prefetch_epochs(h)}};
     for (const auto &kv : keys)
@@ -2830,13 +2805,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->halo_loopback = value;
     }
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
-    else if (k == "yt_mix") { // from the next y-pass enqueued (the list is rebuilt after the queue drains)
-        if (value < 0) return fail(DF_EINVAL, "yt_mix must be >= 0");
-        if (h->device >= 0)
-            if (int rc = sync_all(h)) return rc;
-        h->yt_mix = value;
-        if (int rc = build_ylists(h)) return rc;
-    }
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
         if (value > 1 && (2 * value > h->nsets || h->nsets % value))

@@ -1813,14 +1813,17 @@ __global__ __launch_bounds__(64 * NW) void ypass_tlds_kernel(SweepArgs a, int nr
 // bit-identical to every other form.
 // DBG (timing ablations, wrong sums; DFAMD_YT_DEBUG): 1 no coefficient loads after chunk 0, 4 every row of a
 // wave sums with row 0's window
-template <int R, int NW, int C, int PD, int DBG>
-__device__ __forceinline__ void ypass_t64_body(const SweepArgs &a, dvec2 (&nbuf)[2][C / 2][64], const int tile,
-                                               const int nrb)
+template <int R, int NW, int C, int PD, int DBG = 0>
+__global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
 {
     constexpr int LP = C / (2 * NW); // pairs of chunk rows each wave loads
     static_assert(C % (2 * NW) == 0, "chunk row pairs split evenly over the waves");
+    // noise rows 2p, 2p + 1 of a chunk side by side for each lane: one ds_read_b128 (4 LDS cycles for 1 KiB)
+    // fetches two rows, where the compiler's ds_read2st64_b64 of two separate rows takes 8
+    __shared__ dvec2 nbuf[2][C / 2][64];
     const int lane = threadIdx.x & 63, w = uniform(threadIdx.x >> 6);
-    const int ncol = a.ylist_ncol;
+    const int tile = a.ylist[blockIdx.x];
+    const int nrb = a.ylist_nrb, ncol = a.ylist_ncol;
     const int rb = tile % nrb, ct = (tile / nrb) % ncol, c = tile / (nrb * ncol);
     if (!((a.comps_mask >> c) & 1)) return; // block-uniform
     const int Ny = a.Ny, RB = NW * R, j0 = rb * RB;
@@ -1836,21 +1839,17 @@ __device__ __forceinline__ void ypass_t64_body(const SweepArgs &a, dvec2 (&nbuf)
     // window there is cwin[r] + C i
     int ilo[R];
     unsigned iw[R];
-    // the coefficient windows through the constant address space: uniform loads from it are always scalar ones
-    // (the compiler's no-clobber proof for a global pointer gave up in the mixed kernel's 1-row body)
-    using cptr = const __attribute__((address_space(4))) double *;
-    const cptr tab0 = (cptr)a.tabf;
-    cptr cwin[R];
+    const double *cwin[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         ilo[r] = 1 << 30; // no row: i - ilo is negative, far above iw as unsigned
         iw[r] = 0;
-        cwin[r] = tab0;
+        cwin[r] = a.tabf;
         if (jw + r < Ny) {
             const int N = nst[jw + r], lo = jw + r - N;
             ilo[r] = (lo - mlo) / C; // lo >= mlo
             iw[r] = (unsigned)((jw + r + N - mlo) / C - ilo[r]);
-            cwin[r] = tab0 + a.tabf_off[N] + (mlo - lo); // tap t = m - lo of noise row m at tabf_off[N] + t
+            cwin[r] = a.tabf + a.tabf_off[N] + (mlo - lo); // tap t = m - lo of noise row m at tabf_off[N] + t
         }
     }
     const int col = ct * 64 + lane; // < Pz: a padding column is loaded and summed but never stored
@@ -1893,7 +1892,7 @@ __device__ __forceinline__ void ypass_t64_body(const SweepArgs &a, dvec2 (&nbuf)
     auto cload = [&](int i) {
 #pragma unroll
         for (int r = 0; r < (DBG == 4 ? 1 : R); ++r) {
-            const cptr src = liv[r] ? cwin[r] + i * C : tab0; // tab0: kTabGuard zeros
+            const double *src = liv[r] ? cwin[r] + i * C : a.tabf; // a.tabf: kTabGuard zeros
 #pragma unroll
             for (int q = 0; q < C; ++q) cw[r][q] = src[q];
         }
@@ -1936,35 +1935,14 @@ __device__ __forceinline__ void ypass_t64_body(const SweepArgs &a, dvec2 (&nbuf)
         __syncthreads();
     };
     for (int i = 0; i < nch; i += PD) unroll_to<0, PD>([&](auto K) { step(K, i + decltype(K)::value); });
-    if (col >= a.ylo[c] && col < a.yhi[c]) { // (no lane-dependent return: the mixed kernel's choice stays uniform)
+    if (col < a.ylo[c] || col >= a.yhi[c]) return;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (jw + r >= Ny) continue;
-            double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.yout[c] + col;
-            if (a.ynt_stores) __builtin_nontemporal_store(acc[r], o);
-            else *o = acc[r];
-        }
+    for (int r = 0; r < R; ++r) {
+        if (jw + r >= Ny) continue;
+        double *o = a.rz[c] + (size_t)(jw + r) * a.rz_pitch[c] + a.yout[c] + col;
+        if (a.ynt_stores) __builtin_nontemporal_store(acc[r], o);
+        else *o = acc[r];
     }
-}
-
-template <int R, int NW, int C, int PD, int DBG = 0>
-__global__ __launch_bounds__(64 * NW) void ypass_t64_kernel(SweepArgs a)
-{
-    // noise rows 2p, 2p + 1 of a chunk side by side for each lane: one ds_read_b128 (4 LDS cycles for 1 KiB)
-    // fetches two rows, where the compiler's ds_read2st64_b64 of two separate rows takes 8
-    __shared__ dvec2 nbuf[2][C / 2][64];
-    ypass_t64_body<R, NW, C, PD, DBG>(a, nbuf, a.ylist[blockIdx.x], a.ylist_nrb);
-}
-
-// Mixed rows per wave: the list's first ylist_nh blocks (the heaviest, 1 row per wave: their serial chains are the
-// kernel's floor) and the rest at 2 rows per wave (more taps per noise value read)
-template <int NW, int C, int PD>
-__global__ __launch_bounds__(64 * NW) void ypass_t64_mix_kernel(SweepArgs a)
-{
-    __shared__ dvec2 nbuf[2][C / 2][64];
-    const int b = blockIdx.x, tile = a.ylist[b];
-    if (b < a.ylist_nh) ypass_t64_body<1, NW, C, PD, 0>(a, nbuf, tile, a.ylist_nrb1);
-    else ypass_t64_body<2, NW, C, PD, 0>(a, nbuf, tile, a.ylist_nrb);
 }
 
 template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a, hipStream_t st)
@@ -1983,10 +1961,6 @@ template <int R, bool TABLE> static hipError_t launch_ypass_t(const SweepArgs &a
                 else if (a.ylist_dbg == 1 && a.ylist_R == 2) hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2, 1>), grid, dim3(256), 0, st, a);
                 else if (a.ylist_dbg == 4 && a.ylist_R == 2) hipLaunchKernelGGL((ypass_t64_kernel<2, 4, 16, 2, 4>), grid, dim3(256), 0, st, a);
                 else return hipErrorInvalidValue;
-                return hipGetLastError();
-            }
-            if (a.ylist_nh > 0 && a.ylist_C == 16 && a.ylist_PD == 2) {
-                hipLaunchKernelGGL((ypass_t64_mix_kernel<4, 16, 2>), grid, dim3(256), 0, st, a);
                 return hipGetLastError();
             }
             switch (a.ylist_R * 1000 + a.ylist_C * 10 + a.ylist_PD) {

@@ -155,8 +155,6 @@ struct SweepArgs {
     int ylist_n, ylist_nrb, ylist_ncol, ylist_R, ylist_C, ylist_PD; // R rows per wave, C noise rows per LDS chunk,
                                                                      // PD chunks of noise loads in flight
     int ylist_dbg; // timing only (DFAMD_YT_DEBUG, wrong sums): ypass_t64_kernel's DBG ablations, 0 = none
-    int ylist_nh, ylist_nrb1; // ypass_t64_mix_kernel: its first ylist_nh blocks at 1 row per wave (ylist_nrb1 row
-                              // blocks per column tile), the rest at 2
     // z-pass strip range of one launch: local strip sl in [0, zs_n) is strip zs_lo + sl, plus zs_gap past
     // zs_gap_at (a z-strip plane's edge strips, which read the halo, around the interior ones: the halo
     // exchange runs under the interior launch). Whole plane: 0, nstrips, nstrips, 0.

@@ -2147,6 +2147,7 @@ int build(df_handle *h, const df_config_c *cfg)
     // the reference's grid (+3..4%) and c2 (+12% packed, +29% table) the next generation's K1 inside the K3 launch
     // costs the co-running sweeps and K3 more than the launch it saves (profiles/r6/z)
     h->rng_chain = (long long)h->Ny * h->Nz_loc <= (1ll << 16) ? 1 : 0;
+    if (const char *e = std::getenv("DFAMD_RNG_CHAIN")) h->rng_chain = std::atoi(e) != 0; // (diagnosis)
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
     if (h->yahead || (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb > 1))
         h->nsets = 3 * h->hb;
@@ -2727,6 +2728,7 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
         HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     }
     h->calls_since_load = 0;
+    h->k1_done = -1; // a K1 run ahead inside the last K3 launch started from the old state
     if (h->gen_launched > h->gen_used || h->hb != 1) // the prefetched noise came from the old state: redo it
         return restart_pipeline(h, 1);
     return DF_OK;

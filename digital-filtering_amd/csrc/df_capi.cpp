@@ -1812,6 +1812,9 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
         if ((rc = dalloc_t(h, &h->wave_counts2, (size_t)nb_pad * kWavesPerBlock))) return rc;
         if ((rc = dalloc_t(h, &h->rnext, 2))) return rc;
         if ((rc = dalloc_t(h, &h->rcnt, 2))) return rc;
+        // the blocks-done counters must read zero before the first K1 on rng_stream (dalloc clears on h->stream;
+        // a reused allocation holds old values until then)
+        HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     }
     {
         long long st1 = 0, stw = 0, lo, to;

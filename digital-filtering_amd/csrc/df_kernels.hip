@@ -169,10 +169,9 @@ __device__ void chain_end_step(const RngGeom &g, uint64_t S, int f, const int *c
                                const uint16_t *masks, int nb, int *cnt, RngNext *out, int *err, int *flag)
 {
     const int tid = threadIdx.x, lane = tid & 63;
-    if (tid == 0) {
-        __threadfence(); // this block's counts and flags before its count
-        flag[0] = atomicAdd(cnt, 1) == nb - 1;
-    }
+    __threadfence(); // every thread: its flags and counts reach the device before the block counts itself done
+    __syncthreads();
+    if (tid == 0) flag[0] = atomicAdd(cnt, 1) == nb - 1;
     __syncthreads();
     if (!flag[0] || tid >= 64) return;
     __threadfence(); // every other block's writes are visible past this point

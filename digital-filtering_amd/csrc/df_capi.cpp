@@ -165,14 +165,6 @@ struct df_handle {
     long long *offsets = nullptr;
     long long *part = nullptr; // K2a run totals -> run prefixes (K2b)
     uint16_t *masks = nullptr; // per-thread polar accept flags (K1 -> K3)
-    // rng_chain (fused-plan single-GPU planes): K1's outputs double-buffered by generation parity (these second
-    // copies for odd generations), the end state K1's last block finds (by the parity of the generation it starts)
-    // and K1's blocks-done counters; k1_done: the generation whose K1 already ran inside the previous K3 launch
-    int rng_chain = 0;
-    uint16_t *masks2 = nullptr;
-    int *counts2 = nullptr, *wave_counts2 = nullptr, *rcnt = nullptr;
-    RngNext *rnext = nullptr;
-    long long k1_done = -1;
     int *wave_counts = nullptr; // accepted attempts per wave of each block (K1 -> K2c)
     uint8_t *xbuf = nullptr;    // run generation: the shares' records (group counts, block prefixes, totals)
     WaveTask *tasks = nullptr;  // waves K3 runs (K2c)
@@ -608,15 +600,6 @@ bool run_form_ok(const df_handle *h)
     return h->gen_dense == 2 && h->dense_ready && !fused_plan && h->geom.gen_split == 1;
 }
 
-// rng_chain: each generation's K1 runs inside the previous generation's compacted-K3 launch, its start state found by
-// the previous K1's last block (the reference grid's table call: K1 is 13-15% of it on the RNG's critical chain,
-// profiles/r6/y). One GPU, the fused plan (the compacted K3 plans its own waves), not on trace handles.
-bool chain_ok(const df_handle *h)
-{
-    return h->rng_chain && h->rnext && !h->tracing && !h->group && h->world == 1 && !h->split_count && !h->comm &&
-           h->fuse_plan && h->rng_blocks <= 1024 && !run_form_ok(h);
-}
-
 // allow_run: the run generation may be used (an in-process group takes it only when every strip can, since the
 // strips exchange its share records)
 int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
@@ -655,23 +638,12 @@ int gen_begin(df_handle *h, RngGeom &g, hipStream_t &rs, bool allow_run = true)
         return DF_OK;
     }
     const RngStateDev *in = h->rstate + gen_set(h, gi);
-    g.end_out = nullptr;
-    g.end_cnt = nullptr;
-    g.chain_k3 = 0;
-    const bool chain = chain_ok(h) && g.fused_plan && g.gen_dense != 2;
-    if (chain && h->k1_done == gi) return DF_OK; // this generation's K1 ran inside the previous K3 launch
-    if (chain) { // odd generations' K1 outputs in the second buffers; this K1 also finds the next one's start
-        g.end_out = h->rnext + ((gi + 1) & 1);
-        g.end_cnt = h->rcnt + (gi & 1);
-    }
-    const bool odd = chain && (gi & 1);
     if (!h->split_count)
-        HIP_OR(launch_rng_count(g, in, odd ? h->counts2 : h->counts, odd ? h->wave_counts2 : h->wave_counts,
-                                odd ? h->masks2 : h->masks, 0, h->rng_blocks, h->rng_blocks, rs, h->err_dev),
+        HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, 0, h->rng_blocks, h->rng_blocks, rs),
                DF_EHIP);
     else
         HIP_OR(launch_rng_count(g, in, h->counts, h->wave_counts, h->masks, h->rank * h->rng_chunk, h->rng_chunk,
-                                h->rng_blocks, rs, h->err_dev),
+                                h->rng_blocks, rs),
                DF_EHIP);
     if (g.gen_dense == 2) HIP_OR(launch_rng_share_scan(g, h->counts, h->split_count ? h->rank : 0, rs), DF_EHIP);
     return DF_OK;
@@ -707,30 +679,13 @@ int gen_end(df_handle *h, const RngGeom &g, hipStream_t rs)
     const int nb_scan = h->split_count ? h->rng_chunk * h->world : h->rng_blocks;
     // split counting exchanges counts only: K3 recomputes the accept flags of the waves it runs
     // (g.recount), a sixth or less of all waves on an interior rank of 8
-    if (h->tracing) {
+    if (h->tracing)
         trace(h, TR_K3, tr_stream(rs), gi, gen_set(h, gi), gen_set(h, gi), gen_set(h, gi + 1));
-    } else {
-        RngGeom gg = g;
-        const bool chain = chain_ok(h) && g.fused_plan && g.gen_dense != 2 && !g.recount;
-        const bool odd = chain && (gi & 1), nodd = !(gi & 1);
-        gg.chain_k3 = 0;
-        h->k1_done = -1;
-        if (chain) { // the next generation's K1 in this launch's last nb_plan blocks
-            gg.chain_k3 = h->rng_blocks * gg.gen_split;
-            gg.chain_in = h->rnext + ((gi + 1) & 1);
-            gg.chain_out = h->rnext + (gi & 1);
-            gg.chain_cnt = h->rcnt + ((gi + 1) & 1);
-            gg.chain_counts = nodd ? h->counts2 : h->counts;
-            gg.chain_wave_counts = nodd ? h->wave_counts2 : h->wave_counts;
-            gg.chain_masks = nodd ? h->masks2 : h->masks;
-            h->k1_done = gi + 1;
-        }
-        HIP_OR(launch_rng_finish(gg, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1),
-                                 odd ? h->counts2 : h->counts, odd ? h->wave_counts2 : h->wave_counts, h->offsets,
-                                 h->part, odd ? h->masks2 : h->masks, h->tasks, h->ntasks, h->err_dev, h->rng_blocks,
-                                 nb_scan, rs),
+    else
+        HIP_OR(launch_rng_finish(g, h->rstate + gen_set(h, gi), h->rstate + gen_set(h, gi + 1), h->counts,
+                                 h->wave_counts, h->offsets, h->part, h->masks, h->tasks, h->ntasks, h->err_dev,
+                                 h->rng_blocks, nb_scan, rs),
                DF_EHIP);
-    }
     if (prof_on(h)) ev_record(h, 5, rs);
     if (gen_pos(h, gi) == h->hb - 1) { // the epoch's noise is ready
         Q_OR(q_record(h, h->ev_rng[gen_epoch(h, gi) & 1], rs, gi));
@@ -1806,16 +1761,6 @@ int alloc_rng(df_handle *h, const df_config_c *cfg)
     if ((rc = dalloc_t(h, &h->part, (nb_pad + 1023) / 1024))) return rc;
     if ((rc = dalloc_t(h, &h->masks, (size_t)nb_pad * kRngThreads))) return rc;
     if ((rc = dalloc_t(h, &h->wave_counts, (size_t)nb_pad * kWavesPerBlock))) return rc;
-    if (h->world == 1 && !cfg->comm_id && h->rng_blocks <= 1024) { // rng_chain's second K1 outputs
-        if ((rc = dalloc_t(h, &h->counts2, nb_pad))) return rc;
-        if ((rc = dalloc_t(h, &h->masks2, (size_t)nb_pad * kRngThreads))) return rc;
-        if ((rc = dalloc_t(h, &h->wave_counts2, (size_t)nb_pad * kWavesPerBlock))) return rc;
-        if ((rc = dalloc_t(h, &h->rnext, 2))) return rc;
-        if ((rc = dalloc_t(h, &h->rcnt, 2))) return rc;
-        // the blocks-done counters must read zero before the first K1 on rng_stream (dalloc clears on h->stream;
-        // a reused allocation holds old values until then)
-        HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
-    }
     {
         long long st1 = 0, stw = 0, lo, to;
         record_layout(h->rng_blocks, &st1, &lo, &to);
@@ -2146,11 +2091,6 @@ int build(df_handle *h, const df_config_c *cfg)
     // sweeps for the same VALU slots, and a whole epoch of slack lets it fill the sweeps' gaps (same-box A/B of two
     // builds, 60-call windows: c3 table 0.334-0.338 -> 0.327 ms, c2 table -2%; profiles/r5/r)
     h->hb_conf = h->hb;
-    // rng_chain on launch-bound planes only (c1, 16k cells: -15% packed, -20% table per call, same-handle A/B); on
-    // the reference's grid (+3..4%) and c2 (+12% packed, +29% table) the next generation's K1 inside the K3 launch
-    // costs the co-running sweeps and K3 more than the launch it saves (profiles/r6/z)
-    h->rng_chain = (long long)h->Ny * h->Nz_loc <= (1ll << 16) ? 1 : 0;
-    if (const char *e = std::getenv("DFAMD_RNG_CHAIN")) h->rng_chain = std::atoi(e) != 0; // (diagnosis)
     h->nsets = h->hb > 1 ? 2 * h->hb : 2;
     if (h->yahead || (h->world == 1 && !cfg->comm_id && h->coeff_mode == DF_COEFF_TABLE && h->hb > 1))
         h->nsets = 3 * h->hb;
@@ -2703,7 +2643,6 @@ int df_rng_state(df_handle *h, uint64_t *state, int *saved_flag, double *saved)
 // the next visible step with hand-off batch hb_new; with overlap its generations are enqueued now.
 static int restart_pipeline(df_handle *h, int hb_new)
 {
-    h->k1_done = -1; // a K1 run ahead started from the old stream position
     h->gen_launched = h->gen_used;
     h->gen_base = h->gen_used;
     h->hb = hb_new;
@@ -2731,7 +2670,6 @@ int df_set_rng_state(df_handle *h, uint64_t state, int saved_flag, double saved)
         HIP_OR(hipStreamSynchronize(h->stream), DF_EHIP);
     }
     h->calls_since_load = 0;
-    h->k1_done = -1; // a K1 run ahead inside the last K3 launch started from the old state
     if (h->gen_launched > h->gen_used || h->hb != 1) // the prefetched noise came from the old state: redo it
         return restart_pipeline(h, 1);
     return DF_OK;
@@ -2750,7 +2688,7 @@ int df_get_tuning(df_handle *h, const char *key, int *value)
         {"zwin_W", h->zwin_W}, {"gen_split", h->geom.gen_split}, {"fuse_plan", h->fuse_plan},
         {"handoff_batch", h->hb_conf}, {"gen_dense", h->gen_dense}, {"fast_log", h->geom.fast_log},
         {"rng_replicate", h->rng_replicate}, {"fused_exchange", h->fused_x}, {"halo_overlap", h->halo_overlap},
-        {"halo_ghost", h->ghost}, {"rng_chain", h->rng_chain},
+        {"halo_ghost", h->ghost},
         // read-only: noise sets allocated at create, epochs generated ahead of the one consumed (prefetch_epochs)
         {"noise_sets", h->nsets}, {"prefetch_epochs", prefetch_epochs(h)}};
     for (const auto &kv : keys)
@@ -2867,7 +2805,6 @@ int df_set_tuning(df_handle *h, const char *key, int value)
         h->halo_loopback = value;
     }
     else if (k == "fuse_plan") h->fuse_plan = value != 0;
-    else if (k == "rng_chain") h->rng_chain = value != 0; // from the next generation launched
     else if (k == "handoff_batch") {
         if (value != 1 && value != 2 && value != 4) return fail(DF_EINVAL, "handoff_batch must be 1, 2 or 4");
         if (value > 1 && (2 * value > h->nsets || h->nsets % value))

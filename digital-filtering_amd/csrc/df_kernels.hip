@@ -127,140 +127,16 @@ __device__ __forceinline__ uint32_t lane_accept_bits(const RngGeom &g, uint64_t 
     return bits;
 }
 
-// One attempt block gb of K1 (256 threads): its accept flags, its waves' and its own accept counts.
-__device__ __forceinline__ void count_block(const RngGeom &g, uint64_t S, int gb, int *__restrict__ counts,
-                                            int *__restrict__ wave_counts, uint16_t *__restrict__ masks, int *wsum)
-{
-    const int tid = threadIdx.x, w = tid >> 6;
-    const uint32_t bits = lane_accept_bits(g, S, gb, tid);
-    int cnt = __builtin_popcount(bits);
-    masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
-    if (g.xbuf) { // accepted attempts per group of 64 (one ballot each) into the share's record (run form)
-        const int lane = tid & 63;
-        int mine = 0;
-#pragma unroll
-        for (int m = 0; m < kRngPerThread; ++m) {
-            const int n = __popcll(__ballot((bits >> m) & 1u));
-            mine = lane == m ? n : mine;
-        }
-        const int sh = gb / g.xchunk;
-        if (lane < kRngPerThread)
-            g.xbuf[(size_t)sh * g.xstride + (size_t)(gb - sh * g.xchunk) * 64 + w * kRngPerThread + lane] = (uint8_t)mine;
-    }
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if ((tid & 63) == 0) {
-        wsum[w] = cnt;
-        wave_counts[(size_t)gb * (kRngThreads / 64) + w] = cnt; // the wave's run of 1024 attempts
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int t = 0;
-        for (int ww = 0; ww < kRngThreads / 64; ++ww) t += wsum[ww];
-        counts[gb] = t;
-    }
-    __syncthreads(); // wsum is rewritten by the next iteration
-}
-
-// rng_chain: after its own block, each of the nb K1 blocks counts itself done; the last one finds the attempt of
-// rank A - 1 (the generation's last) from every block's counts and flags and writes the state after that attempt's
-// four outputs - the state K3's last lane writes to the next generation's slot (gen_batch), computed here from the
-// counts alone - and the next generation's cached-normal flag. Vector atomics and fences only.
-__device__ void chain_end_step(const RngGeom &g, uint64_t S, int f, const int *counts, const int *wave_counts,
-                               const uint16_t *masks, int nb, int *cnt, RngNext *out, int *err, int *flag)
-{
-    const int tid = threadIdx.x, lane = tid & 63;
-    __threadfence(); // every thread: its flags and counts reach the device before the block counts itself done
-    __syncthreads();
-    if (tid == 0) flag[0] = atomicAdd(cnt, 1) == nb - 1;
-    __syncthreads();
-    if (!flag[0] || tid >= 64) return;
-    __threadfence(); // every other block's writes are visible past this point
-    const long long A = (long long)((g.Q - (uint64_t)f + 1) / 2);
-    if (A == 0) {
-        if (lane == 0) *out = RngNext{S, (int)((g.Q - (uint64_t)f) & 1u), 0};
-        if (lane == 0) atomicExch(cnt, 0);
-        return;
-    }
-    const long long T = A - 1;
-    // three rounds of independent loads (counts; the chosen block's wave counts; its wave's flags and jumps),
-    // the searches between them in registers and shuffles
-    const volatile int *vc = counts;
-    int c16[16];
-    long long t = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) { // 16 consecutive blocks per lane (nb <= 1024)
-        const int b = lane * 16 + i;
-        c16[i] = b < nb ? vc[b] : 0;
-        t += c16[i];
-    }
-    long long incl = t;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-    }
-    const long long total = __shfl(incl, 63);
-    if (total <= T) { // not enough attempts launched: the host re-sizes (as K3)
-        if (lane == 0) {
-            *err = 1;
-            atomicExch(cnt, 0);
-        }
-        return;
-    }
-    const int L = __builtin_ctzll(__ballot(incl > T)); // the lane whose 16 blocks hold rank T
-    long long r = T - (__shfl(incl, L) - __shfl(t, L));
-    int b = -1;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int ci = __shfl(c16[i], L);
-        if (b < 0) {
-            if (r < ci) b = L * 16 + i;
-            else r -= ci;
-        }
-    }
-    const int wc = lane < kRngThreads / 64 ? ((const volatile int *)wave_counts)[(size_t)b * (kRngThreads / 64) + lane] : 0;
-    int w = -1;
-#pragma unroll
-    for (int i = 0; i < kRngThreads / 64; ++i) {
-        const int ci = __shfl(wc, i);
-        if (w < 0) {
-            if (r < ci) w = i;
-            else r -= ci;
-        }
-    }
-    const uint32_t bits = ((const volatile uint16_t *)masks)[(size_t)b * kRngThreads + w * 64 + lane];
-    const PcgJumpDev jb = g.jump_block[b], jt = g.jump_thread[w * 64 + lane];
-    int m = 0;
-    uint64_t bal = 0;
-    for (; m < kRngPerThread; ++m) {
-        bal = __ballot((bits >> m) & 1u);
-        const int c = __popcll(bal);
-        if (r < c) break;
-        r -= c;
-    }
-    for (long long k = 0; k < r; ++k) bal &= bal - 1;
-    const int L2 = __builtin_ctzll(bal); // the lane of attempt m holding rank T
-    const uint64_t tm = __shfl(jt.mult, L2), tp = __shfl(jt.plus, L2);
-    if (lane == 0) {
-        uint64_t st = tm * (jb.mult * S + jb.plus) + tp; // thread_first_state of that lane
-        for (int k = 0; k < m; ++k) st = g.next_mult * st + g.next_plus;
-        for (int k = 0; k < 4; ++k) st = st * kPcgMult + kPcgInc; // past the attempt's four outputs
-        *out = RngNext{st, (int)((g.Q - (uint64_t)f) & 1u), 0};
-        atomicExch(cnt, 0); // ready for this counter's next generation
-    }
-}
-
 // Counts blocks [b0, b0 + gridDim.x) of the call; blocks >= nb_total (padding of
 // the last z-strip rank's share) report zero.
 // Blocks [b0, b0 + nb) of the call, one workgroup each (the loop strides only if a grid smaller than nb
 // caps how many K1 waves are resident beside the sweeps; 0 = one block per attempt block).
 __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const RngStateDev *__restrict__ sin,
                                                                int *__restrict__ counts, int *__restrict__ wave_counts,
-                                                               uint16_t *__restrict__ masks, int b0, int nb, int nb_total,
-                                                               int *__restrict__ err)
+                                                               uint16_t *__restrict__ masks, int b0, int nb, int nb_total)
 {
-    __shared__ int wsum[kRngThreads / 64 + 1];
-    const int tid = threadIdx.x;
+    __shared__ int wsum[kRngThreads / 64];
+    const int tid = threadIdx.x, w = tid >> 6;
     for (int gb = b0 + blockIdx.x; gb < b0 + nb; gb += gridDim.x) { // block-uniform trip count
         if (gb >= nb_total) {
             if (tid == 0) counts[gb] = 0;
@@ -271,12 +147,34 @@ __global__ __launch_bounds__(kRngThreads) void rng_count_kernel(RngGeom g, const
             }
             continue;
         }
-        count_block(g, sin->state, gb, counts, wave_counts, masks, wsum);
+        const uint32_t bits = lane_accept_bits(g, sin->state, gb, tid);
+        int cnt = __builtin_popcount(bits);
+        masks[(size_t)gb * kRngThreads + tid] = (uint16_t)bits; // accept flags for K3
+        if (g.xbuf) { // accepted attempts per group of 64 (one ballot each) into the share's record (run form)
+            const int lane = tid & 63;
+            int mine = 0;
+#pragma unroll
+            for (int m = 0; m < kRngPerThread; ++m) {
+                const int n = __popcll(__ballot((bits >> m) & 1u));
+                mine = lane == m ? n : mine;
+            }
+            const int sh = gb / g.xchunk;
+            if (lane < kRngPerThread)
+                g.xbuf[(size_t)sh * g.xstride + (size_t)(gb - sh * g.xchunk) * 64 + w * kRngPerThread + lane] = (uint8_t)mine;
+        }
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        if ((tid & 63) == 0) {
+            wsum[w] = cnt;
+            wave_counts[(size_t)gb * (kRngThreads / 64) + w] = cnt; // the wave's run of 1024 attempts
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int t = 0;
+            for (int ww = 0; ww < kRngThreads / 64; ++ww) t += wsum[ww];
+            counts[gb] = t;
+        }
+        __syncthreads(); // wsum is rewritten by the next iteration
     }
-    // rng_chain (one GPU, one block per attempt block): the generation's end state for the next one's K1
-    if (g.end_out)
-        chain_end_step(g, sin->state, sin->saved_flag, counts, wave_counts, masks, gridDim.x, g.end_cnt, g.end_out,
-                       err, wsum + kRngThreads / 64);
 }
 
 // K2: exclusive scan of the per-block accept counts in two levels, so no thread walks a long
@@ -632,24 +530,10 @@ __global__ __launch_bounds__(kRngThreads) void rng_generate_compact_kernel(RngGe
                                                                           int *__restrict__ err)
 {
     __shared__ uint64_t ring_all[kRngThreads / 64][kGenRing];
-    // rng_chain: the launch's first nb_plan blocks run the next generation's K1 (dispatched first, so it overlaps
-    // this generation's K3 blocks behind it); block-uniform
-    int bid = (int)blockIdx.x;
-    if (g.chain_k3 > 0) {
-        if (bid < g.nb_plan) {
-            int *sh = reinterpret_cast<int *>(&ring_all[0][0]);
-            const RngNext nx = *g.chain_in;
-            count_block(g, nx.state, bid, g.chain_counts, g.chain_wave_counts, g.chain_masks, sh);
-            chain_end_step(g, nx.state, nx.f, g.chain_counts, g.chain_wave_counts, g.chain_masks, g.nb_plan,
-                           g.chain_cnt, g.chain_out, err, sh + kRngThreads / 64);
-            return;
-        }
-        bid -= g.nb_plan;
-    }
     const int lane = threadIdx.x & 63;
     uint64_t *ring = ring_all[threadIdx.x >> 6];
     const int split = g.gen_split;
-    const int vslot = uniform(bid * (kRngThreads / 64) + (threadIdx.x >> 6));
+    const int vslot = uniform(blockIdx.x * (kRngThreads / 64) + (threadIdx.x >> 6));
     const int slot = vslot / split, sub = vslot - slot * split;
     const uint64_t f = (uint64_t)sin->saved_flag;
     const long long A = (long long)((g.Q - f + 1) / 2);
@@ -1223,10 +1107,10 @@ hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share,
 }
 
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
-                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st, int *err)
+                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st)
 {
     hipLaunchKernelGGL(rng_count_kernel, dim3(nb), dim3(kRngThreads), 0, st, g, st_in, counts, wave_counts, masks, b0,
-                       nb, nb_total, err);
+                       nb, nb_total);
     return hipGetLastError();
 }
 
@@ -1257,10 +1141,8 @@ hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStat
         hipLaunchKernelGGL(rng_plan_kernel, dim3((nw + 255) / 256), dim3(256), 0, st, g, st_in, offsets, part,
                            wave_counts, nb_total, tasks, ntasks);
     }
-    // (rng_chain: g.chain_k3 = nb_total * gen_split, and nb_plan more blocks, first, run the next generation's K1)
-    const unsigned grid = (unsigned)(nb_total * g.gen_split + (g.chain_k3 > 0 ? g.nb_plan : 0));
-    hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(grid), dim3(kRngThreads), 0, st, g, st_in, st_out, tasks,
-                       ntasks, masks, counts, wave_counts, err);
+    hipLaunchKernelGGL(rng_generate_compact_kernel, dim3(nb_total * g.gen_split), dim3(kRngThreads), 0, st, g,
+                       st_in, st_out, tasks, ntasks, masks, counts, wave_counts, err);
     return hipGetLastError();
 }
 

@@ -68,13 +68,6 @@ struct RunPiece {
     uint32_t c0, li0, n, pad;
 };
 
-// The stream state after a generation's last attempt and the next generation's cached-normal flag, found by K1's
-// last block from the counts (rng_chain): the next generation's K1 can start before this generation's K3 ends.
-struct RngNext {
-    uint64_t state;
-    int f, pad;
-};
-
 struct RngGeom {
     uint64_t seg[7];        // stream order u.r_ys,u.r_zs,v.r_ys,v.r_zs,w.r_ys,w.r_zs
     uint64_t Q;             // normals drawn per call
@@ -117,16 +110,6 @@ struct RngGeom {
     int npieces[2];
     const PcgJumpDev *jump_gi, *jump_lane;
     long long nb_groups; // groups of the call's attempt blocks (64 per block)
-    // Generation chain (rng_chain; fused-plan planes, one GPU). A K1 with end_out set also finds its generation's
-    // end state (its last block, end_cnt counting the blocks done); a compacted K3 launch with chain_k3 > 0 runs the
-    // NEXT generation's K1 in its blocks [chain_k3, chain_k3 + nb_plan): start state chain_in, outputs chain_*.
-    RngNext *end_out;
-    int *end_cnt;
-    int chain_k3;
-    const RngNext *chain_in;
-    RngNext *chain_out;
-    int *chain_cnt, *chain_counts, *chain_wave_counts;
-    uint16_t *chain_masks;
 };
 
 struct SweepArgs {
@@ -196,7 +179,7 @@ hipError_t launch_expand_coeffs(double *B, const long long *off, const int *N_st
                                 hipStream_t st);
 // K1 for blocks [b0, b0+nb) of nb_total (a z-strip rank counts its share only).
 hipError_t launch_rng_count(const RngGeom &g, const RngStateDev *st_in, int *counts, int *wave_counts,
-                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st, int *err);
+                            uint16_t *masks, int b0, int nb, int nb_total, hipStream_t st);
 // K2s (run generation): share `share`'s block prefix and total into its exchange record (after K1).
 hipError_t launch_rng_share_scan(const RngGeom &g, const int *counts, int share, hipStream_t st);
 hipError_t launch_rng_finish(const RngGeom &g, const RngStateDev *st_in, RngStateDev *st_out, int *counts,

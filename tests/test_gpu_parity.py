@@ -195,8 +195,7 @@ def test_golden_native_grid(mode, tuning):
                                          ("table", dict(ylds=3, yt_rows=1)), ("table", dict(ylds=3, yt_rows=2)),
                                          ("table", dict(ylds=3, yt_rows=1, yt_pd=4)), ("table", dict(ylds=3, yt_rows=2, yt_chunk=8)),
                                          ("table", dict(ylds=3, yt_rows=1, yt_chunk=24)),
-                                         ("table", dict(ylds=0)), ("table", dict(rng_chain=1)),
-                                         ("packed", dict(rng_chain=1))])
+                                         ("table", dict(ylds=0))])
 def test_native_grid_bitexact_vs_oracle(mode, tuning):
     # the whole 510 x 400 plane of the reference's grid against the live oracle, bit for bit: the row-pair
     # y-pass (packed default, its 16-column last strip folded 8 noise rows per load) and the table path
@@ -323,8 +322,6 @@ def test_runtime_tuning_is_bitexact(mode):
                 dict(fuse_plan=0, gen_split=1, gen_dense=2),
                 dict(fuse_plan=0), dict(fuse_plan=1, gen_split=4), dict(fuse_plan=0, gen_split=2), dict(fuse_plan=1, gen_split=1),
                 dict(gen_dense=0), dict(handoff_batch=1), dict(handoff_batch=2), dict(handoff_batch=4),
-                dict(rng_chain=0), dict(rng_chain=1), dict(rng_chain=1, handoff_batch=1), dict(rng_chain=0),
-                dict(rng_chain=1, handoff_batch=2), dict(gen_split=2),
                 dict(ylds=1, rows_per_wave=1), dict(ylds=1, rows_per_wave=2), dict(ylds=1, rows_per_wave=4),
                 dict(ylds=1, rows_per_wave=8), dict(ylds=0), dict(ypass_ahead=0), dict(ypass_ahead=1)]
     if mode == "table":  # 64-column tiles (ypass_t64_kernel), every row count, then back

@@ -342,12 +342,8 @@ def test_alloc_registry_rejects_overlapping_ranges():
     (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(rows_per_wave=4, ylds=0, handoff_batch=2)),
     (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "packed",
      dict(rows_per_wave=2, zsplit=1, handoff_batch=2, gen_split=2)),
-    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(gen_split=4, rng_chain=0)),
-    (dict(), "packed", dict(zsplit=0, rng_chain=0)),
-    (dict(), "table", dict(rng_chain=0)),
-    # c1 (16k cells, launch-bound): the next generation's K1 inside the K3 launch (rng_chain)
-    (dict(plane="synthetic", Ny=128, Nz=128, N_min=8, N_max=8), "packed", dict(rng_chain=1, handoff_batch=4)),
-    (dict(plane="synthetic", Ny=128, Nz=128, N_min=8, N_max=8), "table", dict(rng_chain=1)),
+    (dict(plane="synthetic", Ny=512, Nz=512, N_min=4, N_max=32), "table", dict(gen_split=4)),
+    (dict(), "packed", dict(zsplit=0)),
 ])
 def test_launch_plan_defaults(plane, mode, expect):
     # the plane-dependent launch shapes chosen at create time (df_get_tuning on host-only handles): a change to
